@@ -1,0 +1,208 @@
+"""bench.py -- refined SV loci/sec on MI355X (BASELINE.json metric), driver contract.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step = one refinement pass of the HIP engine (svt_refine_device, one batched launch)
+over one rank's shard of SV loci, with the pileup and loci already resident in HBM.
+N>1: every rank owns its own shard (independent loci, no data-path collective: weak
+scaling); each step ends with the one RCCL gather of refined calls to rank 0 that the
+multi-GPU path performs.  Rank 0 prints ONE JSON line.
+
+roofline: algorithmic bytes of the dominant kernel (refine_kernel) per launch =
+  16 B/locus in + 8 B/locus out + Σ_windows Σ_yielded reads (12 B + 4 B × CIGAR words walked)
+(counted exactly by svt_count_work) ÷ the kernel's mean duration,
+measured with HIP events on the launch stream.  cpu_baseline: the CPU oracle
+(restatement of the reference's tpool path over the same in-memory pileup) timed on
+rank 0's host cores on the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(res, n_threads: int, budget_s: float = 20.0) -> dict:
+    """Time the CPU oracle (reference-shaped restatement, T pthread workers) on a bounded
+    sample of the same workload.  Test-infrastructure leg: the only bench use of oracle/."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ffi as O  # noqa: E402
+
+    loci = res.loci
+    # calibrate on a small prefix, then size the sample to ~budget_s of CPU work
+    n0 = min(len(loci), 500)
+    t = time.perf_counter()
+    O.refine_batch(res.pileup, loci[:n0], threads=1)
+    dt = max(time.perf_counter() - t, 1e-6)
+    per_locus_1t = dt / n0
+    n1 = int(min(len(loci), max(n0, budget_s / 3 / per_locus_1t)))
+    t = time.perf_counter()
+    O.refine_batch(res.pileup, loci[:n1], threads=1)
+    v1 = n1 / (time.perf_counter() - t)
+    nt = int(min(len(loci), max(n0, budget_s * 2 / 3 / per_locus_1t * n_threads / 2)))
+    t = time.perf_counter()
+    O.refine_batch(res.pileup, loci[:nt], threads=n_threads)
+    vt = nt / (time.perf_counter() - t)
+    return {
+        "value": round(vt, 1), "unit": "loci/s", "cores": n_threads, "kind": "port",
+        "sample": f"first {nt} loci of the same workload, in-memory columnar pileup (no BGZF inflate), "
+                  f"{n_threads} pthread workers on {_cpu_model()}; 1 thread: {v1:.1f} loci/s on {n1} loci",
+        "value_1thread": round(v1, 1),
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg2_10kdel_30x_ont")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from svtrek_amd import Engine, Params, sim
+    from svtrek_amd._lib import RESULT_DTYPE
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    # ---- synthetic workload (BASELINE config), one shard per rank (weak scaling)
+    cfg = sim.WORKLOADS[args.workload]
+    if world > 1:
+        from dataclasses import replace
+        cfg = replace(cfg, seed=cfg.seed + 1000 * rank)
+    t0 = time.perf_counter()
+    res = sim.generate(cfg)
+    gen_s = time.perf_counter() - t0
+    n = len(res.loci)
+
+    eng = Engine(Params(), device=dev.index)
+    t0 = time.perf_counter()
+    eng.load_pileup(res.pileup)
+    load_s = time.perf_counter() - t0
+    work = eng.count_work(res.loci)   # exact algorithmic work (diagnostic launch, untimed)
+
+    loci_np = res.loci.view("u1").reshape(-1)
+    d_loci = torch.from_numpy(loci_np.copy()).to(dev)
+    d_out = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    gather_list = None
+    if world > 1 and not args.no_gather:
+        gather_list = [torch.empty_like(d_out) for _ in range(world)] if rank == 0 else None
+
+    def step():
+        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), sh)
+        if world > 1 and not args.no_gather:
+            dist.gather(d_out, gather_list, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync(sh)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), sh)
+        ev[i][1].record(stream)
+        if world > 1 and not args.no_gather:
+            dist.gather(d_out, gather_list, dst=0)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    eng.sync(sh)   # raises on a deferred spill-pool overflow
+    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    kern_mean_ms = sum(kern_ms) / len(kern_ms)
+
+    t_max = wall
+    if world > 1:
+        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+
+    total_loci = n * world * args.steps
+    value = total_loci / t_max
+    alg_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
+    achieved = alg_bytes / (kern_mean_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except AttributeError:
+            avail = os.cpu_count() or 1
+        threads = args.cpu_threads or max(1, min(16, avail))
+        cpu = cpu_baseline(res, threads)
+
+    if rank == 0:
+        out = {
+            "metric": "refined SV loci/sec (whole node)",
+            "value": round(value, 1),
+            "unit": "loci/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (seeded simpileup: ONT-like pileup + SV loci; no real BAM)",
+            "config": {"workload": args.workload, "loci_per_gpu": n, "reads_per_gpu": res.pileup.n_reads,
+                       "cigar_ops_per_gpu": res.pileup.n_ops, "coverage": cfg.coverage,
+                       "read_len_mean": cfg.read_len_mean, "parallelism": f"loci-shard x{world}",
+                       "gather": bool(world > 1 and not args.no_gather)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "refine_kernel", "kernel_ms_mean": round(kern_mean_ms, 5),
+                         "kernel_ms_min": round(kern_ms[0], 5), "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "work": work,
+            "setup_s": {"generate": round(gen_s, 2), "load_pileup": round(load_s, 2)},
+            "pileup_device_bytes": eng.device_bytes,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,154 @@
+/*
+ * svtrek_gpu.h -- C ABI of the MI355X SV-refinement engine (the `audt` hot path).
+ *
+ * This header is the drop-in boundary.  The reference has no FFI: its hot path is
+ * three internal C calls made once per VCF record by the worker `thread_func`
+ * (reference audit.c:50-248):
+ *
+ *   void deletion (int chrom, interval begin, interval end, interval sv_inter,
+ *                  t_arg *params, interval *res_inter);          refinement.h:59 / refinement.c:327-330
+ *   void insertion(int chrom, interval begin, uint32_t pos,
+ *                  t_arg *params, uint32_t *res_start);           refinement.h:76 / refinement.c:332-334
+ *   void inversion(int chrom, interval begin, interval end, interval sv_inter,
+ *                  t_arg *params, interval *res_inter);           refinement.h:94 / refinement.c:336-339
+ *
+ * each of which runs htslib region queries (sam_itr_queryi/sam_itr_next,
+ * refinement.c:114-117), a CIGAR walk (refinement.c:103-325) and the consensus vote
+ * (consensus_pos, refinement.c:41-101).  Here the per-record calls become ONE
+ * batched call over many loci (svt_refine_batch / svt_refine_device); the reads the
+ * htslib iterator would yield come from a columnar pileup loaded once
+ * (svt_load_pileup), and the window arithmetic of audit.c:176-232 happens inside
+ * the engine from the parsed record (svt_locus) and the parameters (svt_params =
+ * the six refinement fields of t_arg, params.h:81-87).
+ *
+ * Conventions: plain C types only, no HIP/torch types; every function returns 0
+ * (SVT_OK) or a negative svt_status; no exceptions cross the ABI.  One svt_ctx
+ * drives one GPU and is used by one host thread at a time; several GPUs = several
+ * contexts (one process per GPU in the multi-GPU driver).  Results use the
+ * reference's encoding: a breakpoint the vote could not refine is 0xFFFFFFFF
+ * (refinement.c returns -1, stored into uint32 at audit.c:179,194).
+ */
+#ifndef SVTREK_GPU_H
+#define SVTREK_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t svt_status;
+#define SVT_OK        0
+#define SVT_EINVAL   -1   /* bad argument (NULL, min_count < 1, malformed pileup)   */
+#define SVT_EDEVICE  -2   /* HIP runtime error (no device, launch failure)           */
+#define SVT_ENOMEM   -3   /* device or host allocation failed                        */
+#define SVT_ESTATE   -4   /* call out of order (refine before load_pileup)           */
+#define SVT_EOVERFLOW -5  /* candidate spill pool exhausted; raise spill_bytes       */
+
+/* SV type codes: identical values to the reference's sv_type_t (params.h:113-121). */
+#define SVT_UNKNOWN 0
+#define SVT_INS     1
+#define SVT_DEL     2
+#define SVT_INV     3
+#define SVT_DUP     4
+#define SVT_TRA     5
+#define SVT_BND     6
+
+#define SVT_NA 0xFFFFFFFFu        /* "not refined" (printed as NA, audit.c:181,197)   */
+
+/* Refinement knobs -- the t_arg fields of params.h:81-87; defaults params.h:27-32. */
+typedef struct svt_params {
+    int32_t wider_interval;            /* --wider-interval            (20000) */
+    int32_t median_interval;           /* --median-interval           (10000) */
+    int32_t narrow_interval;           /* --narrow-interval           ( 2000) */
+    int32_t consensus_interval_range;  /* --consensus-interval-range  (  500) */
+    int32_t consensus_interval;        /* --consensus-interval        (    5) */
+    int32_t consensus_min_count;       /* --consensus-min-count       (    3), must be >= 1 */
+    uint64_t spill_bytes;              /* device pool for windows with > SVT_LDS_CANDS
+                                          candidates; 0 = default (64 MiB)            */
+} svt_params;
+
+/* One parsed VCF record as it reaches the type switch of audit.c:175.
+ * chrom = chrom_index of audit.c:101-105 (the BAM tid is chrom-1, refinement.c:114);
+ * pos/end are the uint32 values of audit.c:108 and audit.c:159/165. */
+typedef struct svt_locus {
+    int32_t  type;   /* SVT_INS / SVT_DEL / SVT_INV (others yield NA/NA)           */
+    int32_t  chrom;
+    uint32_t pos;
+    uint32_t end;
+} svt_locus;
+
+/* Refined breakpoints.  DEL: {refine_start, refine_end}; INS: {refine_ins, NA};
+ * INV: {refine_point, refine_point} (always NA, refinement.c:250). */
+typedef struct svt_result {
+    uint32_t start;
+    uint32_t end;
+} svt_result;
+
+/* Soft-clip tests the reference makes on every yielded read, precomputed at ingest so
+ * reads with n_cigar == 0 keep the bytes the reference actually tests
+ * (refinement.c:120 reads cigar[n_cigar-1], refinement.c:210 reads cigar[0]). */
+#define SVT_CLIP_LAST_S  0x1u   /* bam_cigar_op(cigar[n_cigar-1]) == S  */
+#define SVT_CLIP_FIRST_S 0x2u   /* bam_cigar_op(cigar[0])         == S  */
+
+/* Caller-owned columnar pileup: the records htslib's iterator can yield, i.e. every
+ * BAM record with tid >= 0 (no flag filtering, reference params.h:23-25 unused).
+ * Reads of contig t are [tid_off[t], tid_off[t+1]) and are sorted by pos. */
+typedef struct svt_pileup_view {
+    int32_t         n_targets;
+    const int64_t  *tid_off;    /* [n_targets+1]                                       */
+    const int32_t  *pos;        /* [n_reads] bam1_core_t.pos (0-based)                  */
+    const int32_t  *endpos;     /* [n_reads] htslib bam_endpos(): pos + max(1, rlen)    */
+    const uint64_t *cig_off;    /* [n_reads+1] read r owns cigar[cig_off[r]..cig_off[r+1]) */
+    const uint32_t *cigar;      /* BAM-packed ops, len << 4 | op                        */
+    const uint8_t  *clip;       /* [n_reads] SVT_CLIP_* bits, or NULL: derive from cigar */
+} svt_pileup_view;
+
+/* Work counters of one batch (svt_count_work): what the reference algorithm touches. */
+typedef struct svt_work {
+    uint64_t windows;        /* region queries issued (INV windows excluded)             */
+    uint64_t reads;          /* reads yielded by the region queries                      */
+    uint64_t ops_walked;     /* CIGAR words consumed by the walk loops, incl. the break op,
+                                plus the soft-clip test word when not already walked      */
+    uint64_t candidates;     /* breakpoint candidates pushed                              */
+    uint64_t spilled_windows;/* windows whose candidates exceeded SVT_LDS_CANDS          */
+} svt_work;
+
+typedef struct svt_ctx svt_ctx;
+
+/* Open a context on HIP device `device` (-1 = current).  Validates params. */
+svt_status svt_open(const svt_params *params, int device, svt_ctx **out);
+
+/* Copy the pileup to device HBM (replaces any previous one).  Synchronous. */
+svt_status svt_load_pileup(svt_ctx *ctx, const svt_pileup_view *pileup);
+
+/* Refine n host-resident loci into host-resident out[n].  Synchronous. */
+svt_status svt_refine_batch(svt_ctx *ctx, const svt_locus *loci, size_t n, svt_result *out);
+
+/* Refine n DEVICE-resident loci into DEVICE-resident out[n] on `hip_stream`
+ * (a hipStream_t passed as void*, NULL = default stream).  Asynchronous: errors of
+ * the launch itself are returned; spill-pool overflow is reported by svt_sync. */
+svt_status svt_refine_device(svt_ctx *ctx, const svt_locus *d_loci, size_t n,
+                             svt_result *d_out, void *hip_stream);
+
+/* Wait for `hip_stream` and report a deferred error (SVT_EOVERFLOW) of earlier calls. */
+svt_status svt_sync(svt_ctx *ctx, void *hip_stream);
+
+/* Count the reference algorithm's work for n host loci (diagnostic, synchronous). */
+svt_status svt_count_work(svt_ctx *ctx, const svt_locus *loci, size_t n, svt_work *out);
+
+/* Bytes of device memory the loaded pileup occupies. */
+uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
+
+const char *svt_last_error(const svt_ctx *ctx);
+void        svt_close(svt_ctx *ctx);
+const char *svt_version(void);
+
+/* LDS candidate capacity per window; larger windows spill to the device pool. */
+#define SVT_LDS_CANDS 512
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVTREK_GPU_H */

@@ -1,0 +1,124 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so (the CPU parity oracle).
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class OrcParams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("wider_interval", "median_interval", "narrow_interval",
+                                          "consensus_interval_range", "consensus_interval",
+                                          "consensus_min_count")]
+
+
+class OrcPileup(C.Structure):
+    _fields_ = [("n_targets", C.c_int32), ("tid_off", C.c_void_p), ("pos", C.c_void_p),
+                ("endpos", C.c_void_p), ("cig_off", C.c_void_p), ("cigar", C.c_void_p), ("clip", C.c_void_p)]
+
+
+class OrcWork(C.Structure):
+    _fields_ = [("windows", C.c_uint64), ("reads", C.c_uint64), ("ops_walked", C.c_uint64),
+                ("candidates", C.c_uint64)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle not built: {path}")
+        L = C.CDLL(path)
+        P = C.c_void_p
+        L.orc_consensus_pos.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_consensus_pos.restype = C.c_int
+        L.orc_lower_bound.argtypes = [P, C.c_int, C.c_int]
+        L.orc_upper_bound.argtypes = [P, C.c_int, C.c_int]
+        for fn in ("orc_refine_start", "orc_refine_end", "orc_refine_point"):
+            getattr(L, fn).argtypes = [P, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+            getattr(L, fn).restype = C.c_int
+        L.orc_refine_ins.argtypes = [P, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+        L.orc_refine_ins.restype = C.c_int
+        L.orc_refine_batch.argtypes = [P, P, P, C.c_size_t, P, C.c_int, P]
+        L.orc_refine_batch.restype = C.c_int
+        L.orc_parse_line.argtypes = [C.c_char_p, P, C.c_char_p, C.c_size_t]
+        L.orc_parse_line.restype = C.c_int
+        L.orc_format_result.argtypes = [P, P, C.c_char_p, C.c_size_t]
+        L.orc_format_result.restype = C.c_int
+        L.orc_audit_text.argtypes = [C.c_char_p, C.c_size_t, P, P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        L.orc_audit_text.restype = C.c_int
+        L.orc_free.argtypes = [P]
+        _lib = L
+    return _lib
+
+
+def params(p=None) -> OrcParams:
+    if p is None:
+        return OrcParams(20000, 10000, 2000, 500, 5, 3)
+    return OrcParams(p.wider_interval, p.median_interval, p.narrow_interval, p.consensus_interval_range,
+                     p.consensus_interval, p.consensus_min_count)
+
+
+def pileup(pl) -> tuple[OrcPileup, list]:
+    keep = [pl.tid_off, pl.pos, pl.endpos, pl.cig_off, pl.cigar, pl.clip]
+    v = OrcPileup(pl.n_targets, pl.tid_off.ctypes.data, pl.pos.ctypes.data, pl.endpos.ctypes.data,
+                  pl.cig_off.ctypes.data, pl.cigar.ctypes.data,
+                  pl.clip.ctypes.data if pl.clip is not None else None)
+    return v, keep
+
+
+def consensus_pos(locs, pos: int, min_count: int = 3, ci: int = 5, rng: int = 500) -> int:
+    a = np.ascontiguousarray(np.array(locs, dtype=np.int32))
+    return lib().orc_consensus_pos(a.ctypes.data if len(a) else None, len(a), pos, min_count, ci, rng)
+
+
+def refine_batch(pl, loci: np.ndarray, prm=None, threads: int = 1, with_work: bool = False):
+    from svtrek_amd._lib import RESULT_DTYPE
+    v, keep = pileup(pl)
+    pr = params(prm)
+    loci = np.ascontiguousarray(loci)
+    out = np.empty(len(loci), dtype=RESULT_DTYPE)
+    w = OrcWork()
+    rc = lib().orc_refine_batch(C.byref(v), C.byref(pr), loci.ctypes.data, len(loci), out.ctypes.data,
+                                threads, C.byref(w))
+    if rc != 0:
+        raise RuntimeError("orc_refine_batch failed")
+    del keep
+    if with_work:
+        return out, {f: int(getattr(w, f)) for f, _ in OrcWork._fields_}
+    return out
+
+
+def parse_line(line: str):
+    """-> (action, (type, chrom, pos, end) or None, err)"""
+    from svtrek_amd._lib import LOCUS_DTYPE
+    buf = C.create_string_buffer(line.encode("latin-1"))
+    loc = np.zeros(1, dtype=LOCUS_DTYPE)
+    err = C.create_string_buffer(512)
+    act = lib().orc_parse_line(buf, loc.ctypes.data, err, 512)
+    rec = tuple(int(x) for x in loc[0]) if act == 1 else None
+    return act, rec, err.value.decode("latin-1")
+
+
+def audit_text(vcf_text: str, pl, prm=None) -> str:
+    v, keep = pileup(pl)
+    pr = params(prm)
+    data = vcf_text.encode("latin-1")
+    out = C.c_void_p()
+    n = C.c_size_t()
+    rc = lib().orc_audit_text(data, len(data), C.byref(v), C.byref(pr), C.byref(out), C.byref(n))
+    if rc != 0:
+        raise RuntimeError("orc_audit_text failed")
+    s = C.string_at(out, n.value).decode("latin-1")
+    lib().orc_free(out)
+    del keep
+    return s

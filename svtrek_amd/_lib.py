@@ -1,0 +1,144 @@
+"""ctypes bindings of the product libraries (C ABI in include/svtrek_gpu.h).
+
+The engine library must exist: there is no CPU fallback anywhere in the product
+path -- a missing or unloadable libsvtrek_hip.so raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+
+SVT_OK = 0
+SVT_EINVAL = -1
+SVT_EDEVICE = -2
+SVT_ENOMEM = -3
+SVT_ESTATE = -4
+SVT_EOVERFLOW = -5
+STATUS_NAMES = {0: "OK", -1: "EINVAL", -2: "EDEVICE", -3: "ENOMEM", -4: "ESTATE", -5: "EOVERFLOW"}
+
+SVT_UNKNOWN, SVT_INS, SVT_DEL, SVT_INV, SVT_DUP, SVT_TRA, SVT_BND = range(7)
+SVT_NA = 0xFFFFFFFF
+SVT_LDS_CANDS = 512
+
+LOCUS_DTYPE = np.dtype([("type", "<i4"), ("chrom", "<i4"), ("pos", "<u4"), ("end", "<u4")])
+RESULT_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4")])
+
+
+class SvtParams(C.Structure):
+    _fields_ = [
+        ("wider_interval", C.c_int32),
+        ("median_interval", C.c_int32),
+        ("narrow_interval", C.c_int32),
+        ("consensus_interval_range", C.c_int32),
+        ("consensus_interval", C.c_int32),
+        ("consensus_min_count", C.c_int32),
+        ("spill_bytes", C.c_uint64),
+    ]
+
+
+class SvtPileupView(C.Structure):
+    _fields_ = [
+        ("n_targets", C.c_int32),
+        ("tid_off", C.c_void_p),
+        ("pos", C.c_void_p),
+        ("endpos", C.c_void_p),
+        ("cig_off", C.c_void_p),
+        ("cigar", C.c_void_p),
+        ("clip", C.c_void_p),
+    ]
+
+
+class SvtWork(C.Structure):
+    _fields_ = [
+        ("windows", C.c_uint64),
+        ("reads", C.c_uint64),
+        ("ops_walked", C.c_uint64),
+        ("candidates", C.c_uint64),
+        ("spilled_windows", C.c_uint64),
+    ]
+
+
+# every symbol include/svtrek_gpu.h declares
+ENGINE_SYMBOLS = (
+    "svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
+    "svt_count_work", "svt_pileup_device_bytes", "svt_last_error", "svt_close", "svt_version",
+)
+
+_engine = None
+
+
+def engine_path() -> str:
+    return os.path.join(PKG, "libsvtrek_hip.so")
+
+
+def load_engine() -> C.CDLL:
+    """Load libsvtrek_hip.so (raises if it is missing: no fallback path exists)."""
+    global _engine
+    if _engine is not None:
+        return _engine
+    path = engine_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"svtrek_amd HIP engine not built: {path} (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    P = C.c_void_p
+    lib.svt_open.argtypes = [C.POINTER(SvtParams), C.c_int, C.POINTER(P)]
+    lib.svt_load_pileup.argtypes = [P, C.POINTER(SvtPileupView)]
+    lib.svt_refine_batch.argtypes = [P, P, C.c_size_t, P]
+    lib.svt_refine_device.argtypes = [P, P, C.c_size_t, P, P]
+    lib.svt_sync.argtypes = [P, P]
+    lib.svt_count_work.argtypes = [P, P, C.c_size_t, C.POINTER(SvtWork)]
+    lib.svt_pileup_device_bytes.argtypes = [P]
+    lib.svt_pileup_device_bytes.restype = C.c_uint64
+    lib.svt_last_error.argtypes = [P]
+    lib.svt_last_error.restype = C.c_char_p
+    lib.svt_close.argtypes = [P]
+    lib.svt_close.restype = None
+    lib.svt_version.restype = C.c_char_p
+    for name in ("svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
+                 "svt_count_work"):
+        getattr(lib, name).restype = C.c_int32
+    _engine = lib
+    return lib
+
+
+_sim = None
+
+
+def load_sim() -> C.CDLL:
+    global _sim
+    if _sim is not None:
+        return _sim
+    path = os.path.join(PKG, "libsvtrek_sim.so")
+    if not os.path.exists(path):
+        raise RuntimeError(f"simulator not built: {path} (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    P = C.c_void_p
+    lib.sim_generate.argtypes = [P]
+    lib.sim_generate.restype = P
+    lib.sim_free.argtypes = [P]
+    lib.sim_free.restype = None
+    for name, rt in (("sim_n_targets", C.c_int32), ("sim_n_reads", C.c_int64), ("sim_n_ops", C.c_uint64),
+                     ("sim_n_loci", C.c_int32)):
+        getattr(lib, name).argtypes = [P]
+        getattr(lib, name).restype = rt
+    lib.sim_contig_len.argtypes = [P, C.c_int32]
+    lib.sim_contig_len.restype = C.c_int32
+    for name in ("sim_tid_off", "sim_pos", "sim_endpos", "sim_cig_off", "sim_cigar", "sim_flag", "sim_loci",
+                 "sim_truth"):
+        getattr(lib, name).argtypes = [P]
+        getattr(lib, name).restype = P
+    lib.sim_write_bam.argtypes = [P, C.c_char_p, C.c_int, C.c_int]
+    lib.sim_write_bam.restype = C.c_int
+    _sim = lib
+    return lib
+
+
+def ptr(a: np.ndarray | None) -> int | None:
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed over the C ABI must be C-contiguous"
+    return a.ctypes.data

@@ -1,0 +1,106 @@
+"""In-tree build of every native artefact (gfx950 HIP engine, host tools, CLI).
+
+Outputs land next to their sources inside the repo so they travel to the GPU box
+with the gpurun snapshot (they are git-ignored, not gpurun-ignored):
+
+    svtrek_amd/libsvtrek_hip.so   HIP kernels + C ABI (include/svtrek_gpu.h)   [product]
+    svtrek_amd/libsvtrek_host.so  BAM ingest + VCF parse/format (C++)          [product]
+    svtrek_amd/svtrek             `svtrek audt` drop-in CLI                     [product]
+    svtrek_amd/libsvtrek_sim.so   seeded synthetic pileups + BAM writer         [test/bench data]
+    oracle/liboracle.so           CPU parity oracle                             [test infra]
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "svtrek_amd")
+CSRC = os.path.join(PKG, "csrc")
+INC = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SVT_OFFLOAD_ARCH", "gfx950")
+
+
+def _run(cmd: list[str], cwd: str | None = None) -> None:
+    r = subprocess.run(cmd, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+
+
+def _stale(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_engine(force: bool = False) -> str:
+    out = os.path.join(PKG, "libsvtrek_hip.so")
+    deps = [os.path.join(CSRC, "svt_engine.hip"), os.path.join(INC, "svtrek_gpu.h")]
+    if force or _stale(out, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-Wall", "-I", INC, "-o", out, deps[0]])
+    return out
+
+
+def build_host(force: bool = False) -> str:
+    out = os.path.join(PKG, "libsvtrek_host.so")
+    srcs = [os.path.join(CSRC, f) for f in ("bam_ingest.cpp", "vcf_audit.cpp")]
+    hdrs = [os.path.join(CSRC, "svtrek_host.h"), os.path.join(INC, "svtrek_gpu.h")]
+    if all(os.path.exists(s) for s in srcs) and (force or _stale(out, srcs + hdrs)):
+        _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-pthread",
+              "-I", INC, "-o", out] + srcs + ["-lz"])
+    return out
+
+
+def build_cli(force: bool = False) -> str:
+    out = os.path.join(PKG, "svtrek")
+    main = os.path.join(CSRC, "svtrek_main.cpp")
+    srcs = [main] + [os.path.join(CSRC, f) for f in ("bam_ingest.cpp", "vcf_audit.cpp")]
+    hdrs = [os.path.join(CSRC, "svtrek_host.h"), os.path.join(INC, "svtrek_gpu.h")]
+    eng = os.path.join(PKG, "libsvtrek_hip.so")
+    if all(os.path.exists(s) for s in srcs) and (force or _stale(out, srcs + hdrs + [eng])):
+        _run(["g++", "-O3", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-I", INC, "-o", out] + srcs +
+             ["-L", PKG, "-lsvtrek_hip", "-Wl,-rpath,$ORIGIN", "-lz"])
+    return out
+
+
+def build_sim(force: bool = False) -> str:
+    out = os.path.join(PKG, "libsvtrek_sim.so")
+    deps = [os.path.join(CSRC, "simpileup.c"), os.path.join(CSRC, "simpileup.h")]
+    if force or _stale(out, deps):
+        _run(["gcc", "-O3", "-std=gnu11", "-fPIC", "-shared", "-Wall", "-Wextra", "-o", out, deps[0],
+              "-lz", "-lm"])
+    return out
+
+
+def build_oracle(force: bool = False) -> str:
+    """Test infrastructure: the CPU parity oracle (oracle/Makefile)."""
+    out = os.path.join(ROOT, "oracle", "liboracle.so")
+    src = [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "svtrek_oracle.h")]
+    if force or _stale(out, src):
+        _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + (["-B"] if force else []))
+    return out
+
+
+def build_all(force: bool = False) -> dict[str, str]:
+    arts = {
+        "engine": build_engine(force),
+        "sim": build_sim(force),
+        "oracle": build_oracle(force),
+    }
+    if os.path.exists(os.path.join(CSRC, "svtrek_main.cpp")):
+        arts["host"] = build_host(force)
+        arts["cli"] = build_cli(force)
+    return arts
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    for k, v in build_all(force).items():
+        print(f"{k:7s} {v} {'ok' if os.path.exists(v) else 'MISSING'}")
+    if shutil.which(HIPCC) is None and not os.path.exists(HIPCC):
+        print("warning: hipcc not found", file=sys.stderr)

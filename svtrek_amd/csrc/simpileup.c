@@ -1,0 +1,541 @@
+/*
+ * simpileup.c -- seeded synthetic long-read pileups + BAM writer (see simpileup.h).
+ *
+ * Deterministic for a given sim_config (xoshiro256** PRNG, no libc rand), so tests on
+ * this container and runs on the GPU box see identical inputs.  Output is columnar and
+ * per-contig sorted by pos, exactly the svt_pileup_view layout (include/svtrek_gpu.h).
+ */
+#include "simpileup.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+enum { OP_M = 0, OP_I = 1, OP_D = 2, OP_N = 3, OP_S = 4, OP_H = 5, OP_P = 6, OP_EQ = 7, OP_X = 8 };
+
+/* ---------------------------------------------------------------- PRNG */
+typedef struct { uint64_t s[4]; } rng_t;
+static uint64_t splitmix(uint64_t *x) {
+    uint64_t z = (*x += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+static void rng_seed(rng_t *r, uint64_t seed) {
+    for (int i = 0; i < 4; i++) r->s[i] = splitmix(&seed);
+}
+static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+static inline uint64_t rng_u64(rng_t *r) {
+    uint64_t *s = r->s, res = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+    s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3]; s[2] ^= t; s[3] = rotl(s[3], 45);
+    return res;
+}
+static inline double rng_unif(rng_t *r) { return (double)(rng_u64(r) >> 11) * (1.0 / 9007199254740992.0); }
+static inline int32_t rng_int(rng_t *r, int32_t lo, int32_t hi) {   /* inclusive */
+    return lo + (int32_t)(rng_u64(r) % (uint64_t)(hi - lo + 1));
+}
+static inline double rng_norm(rng_t *r) {
+    double u1 = rng_unif(r), u2 = rng_unif(r);
+    if (u1 < 1e-300) u1 = 1e-300;
+    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+static inline int32_t rng_geom(rng_t *r, double mean) {
+    double u = rng_unif(r);
+    if (u < 1e-300) u = 1e-300;
+    int32_t v = (int32_t)(-log(u) * mean) + 1;
+    return v < 1 ? 1 : v;
+}
+
+/* ---------------------------------------------------------------- storage */
+typedef struct { int32_t type, chrom, pos, end, bp1, bp2, tid; } locus_t;
+
+struct sim_pileup {
+    int32_t   n_targets;
+    int32_t  *contig_len;
+    int64_t   n_reads;
+    uint64_t  n_ops;
+    int64_t  *tid_off;
+    int32_t  *pos, *endpos;
+    uint64_t *cig_off;
+    uint32_t *cigar;
+    uint16_t *flag;
+    int32_t   n_loci;
+    int32_t  *loci;    /* type, chrom, pos, end */
+    int32_t  *truth;   /* bp1, bp2 */
+};
+
+typedef struct {           /* unsorted read list while generating */
+    int32_t  *pos;  uint16_t *flag; uint64_t *off; int32_t *tid;
+    int64_t   n, cap;
+    uint32_t *ops;  uint64_t nops, capops;
+} rbuf;
+
+static int rb_reserve_ops(rbuf *b, uint64_t extra) {
+    if (b->nops + extra <= b->capops) return 0;
+    uint64_t nc = b->capops ? b->capops : (1u << 20);
+    while (nc < b->nops + extra) nc *= 2;
+    uint32_t *x = (uint32_t *)realloc(b->ops, nc * sizeof(uint32_t));
+    if (!x) return -1;
+    b->ops = x; b->capops = nc;
+    return 0;
+}
+static int rb_begin(rbuf *b, int32_t tid, int32_t pos, uint16_t flag) {
+    if (b->n == b->cap) {
+        int64_t nc = b->cap ? b->cap * 2 : 4096;
+        int32_t *p = (int32_t *)realloc(b->pos, (size_t)nc * sizeof(int32_t));
+        if (!p) return -1;
+        b->pos = p;
+        uint16_t *f = (uint16_t *)realloc(b->flag, (size_t)nc * sizeof(uint16_t));
+        if (!f) return -1;
+        b->flag = f;
+        uint64_t *o = (uint64_t *)realloc(b->off, (size_t)(nc + 1) * sizeof(uint64_t));
+        if (!o) return -1;
+        b->off = o;
+        int32_t *t = (int32_t *)realloc(b->tid, (size_t)nc * sizeof(int32_t));
+        if (!t) return -1;
+        b->tid = t;
+        b->cap = nc;
+    }
+    b->pos[b->n] = pos; b->flag[b->n] = flag; b->tid[b->n] = tid; b->off[b->n] = b->nops;
+    return 0;
+}
+static inline void rb_op(rbuf *b, uint32_t op, uint32_t len) {
+    if (len == 0) return;
+    /* merge with the previous op of the same read when identical (keeps CIGARs canonical) */
+    if (b->nops > b->off[b->n] && (b->ops[b->nops - 1] & 0xf) == op && op != OP_S && op != OP_H) {
+        b->ops[b->nops - 1] += len << 4;
+        return;
+    }
+    b->ops[b->nops++] = (len << 4) | op;
+}
+static inline void rb_end(rbuf *b) { b->n++; b->off[b->n] = b->nops; }
+
+/* ---------------------------------------------------------------- read model */
+typedef struct {
+    const sim_config *c;
+    rng_t *r;
+    rbuf *b;
+    const locus_t *sv; int32_t nsv;   /* SVs of this contig sorted by bp1 */
+    int32_t tid, clen;
+} gen_t;
+
+static void small_event(gen_t *g, int32_t *ref, int32_t *q) {
+    rng_t *r = g->r;
+    double u = rng_unif(r);
+    if (g->c->p_exotic > 0 && rng_unif(r) < g->c->p_exotic) {
+        int32_t k = rng_int(r, 0, 5);
+        uint32_t op = k == 0 ? OP_N : k == 1 ? OP_H : k == 2 ? OP_P : (uint32_t)rng_int(r, 9, 15);
+        int32_t len = rng_int(r, 1, 60);
+        rb_op(g->b, op, (uint32_t)len);
+        /* the reference walk advances rp on every op but I and S (refinement.c:141) */
+        *ref += len;
+        return;
+    }
+    int32_t len = rng_int(r, 1, 5);
+    if (u < 0.40) { rb_op(g->b, OP_X, (uint32_t)len); *ref += len; *q -= len; }
+    else if (u < 0.70) { rb_op(g->b, OP_I, (uint32_t)len); *q -= len; }
+    else { rb_op(g->b, OP_D, (uint32_t)len); *ref += len; }
+}
+
+/* Build one read starting at `start`, query length `qlen`.  Emits the primary (and a
+ * supplementary for split reads).  Returns 0 / -1 on OOM. */
+static int make_read(gen_t *g, int32_t start, int32_t qlen, int32_t *sv_cursor) {
+    const sim_config *c = g->c;
+    rng_t *r = g->r;
+    rbuf *b = g->b;
+    if (rb_reserve_ops(b, 3ull * (uint64_t)qlen + 16)) return -1;   /* <= 3 ops per loop turn, >= 1 base each */
+    if (rb_begin(b, g->tid, start, 0)) return -1;
+    int32_t ref = start, q = qlen;
+    /* leading clip */
+    if (rng_unif(r) < c->p_clip_ends) {
+        int32_t k = rng_int(r, 1, 200);
+        rb_op(b, rng_unif(r) < 0.8 ? OP_S : OP_H, (uint32_t)k);
+    }
+    int noise_done = rng_unif(r) >= c->p_noise_sv;
+    int32_t cur = *sv_cursor;
+    while (cur < g->nsv && g->sv[cur].bp1 < start) cur++;   /* first SV at/after read start */
+    double mean_m = c->rho > 0 ? 2.0 / c->rho : 1e9;   /* each error event = M + op: rho ops/bp */
+    int split = 0;
+    int32_t split_ref = 0, split_q = 0;
+    while (q > 0 && ref < g->clen - 1) {
+        int32_t m = rng_geom(r, mean_m);
+        if (m > q) m = q;
+        if (cur < g->nsv && ref + m >= g->sv[cur].bp1) {
+            const locus_t *sv = &g->sv[cur];
+            int32_t j1 = c->bp_jitter ? rng_int(r, -c->bp_jitter, c->bp_jitter) : 0;
+            int32_t bp1 = sv->bp1 + j1;
+            if (bp1 <= ref) bp1 = ref + 1;
+            int32_t mm = bp1 - ref;
+            if (mm > q) { rb_op(b, OP_M, (uint32_t)q); ref += q; q = 0; break; }
+            rb_op(b, OP_M, (uint32_t)mm); ref += mm; q -= mm;
+            cur++;
+            double u = rng_unif(r);
+            if (sv->type == 2) {           /* DEL */
+                int32_t j2 = c->bp_jitter ? rng_int(r, -c->bp_jitter, c->bp_jitter) : 0;
+                int32_t dl = sv->bp2 + j2 - bp1;
+                if (dl < 1) dl = 1;
+                if (u < c->p_split) {
+                    split = 1; split_ref = ref + dl; split_q = q;
+                    rb_op(b, OP_S, (uint32_t)(q > 0 ? q : 1));
+                    q = 0;
+                    break;
+                } else if (u < c->p_split + c->p_carry) {
+                    rb_op(b, OP_D, (uint32_t)dl); ref += dl;
+                }
+            } else {                       /* INS */
+                int32_t il = sv->bp2 - sv->bp1;
+                if (il < 1) il = 1;
+                if (u < c->p_carry) { rb_op(b, OP_I, (uint32_t)il); q -= il < q ? il : q; }
+            }
+            continue;
+        }
+        rb_op(b, OP_M, (uint32_t)m); ref += m; q -= m;
+        if (q <= 0) break;
+        if (!noise_done && rng_unif(r) < 0.01) {
+            noise_done = 1;
+            int32_t len = rng_int(r, 45, 400);
+            if (rng_unif(r) < 0.5) { rb_op(b, OP_D, (uint32_t)len); ref += len; }
+            else { rb_op(b, OP_I, (uint32_t)len); q -= len; }
+            continue;
+        }
+        small_event(g, &ref, &q);
+    }
+    if (!split && rng_unif(r) < c->p_clip_ends) {
+        int32_t k = rng_int(r, 1, 200);
+        rb_op(b, rng_unif(r) < 0.8 ? OP_S : OP_H, (uint32_t)k);
+    }
+    if (b->nops == b->off[b->n]) rb_op(b, OP_M, 1);   /* never emit n_cigar == 0 */
+    rb_end(b);
+    if (split && split_ref < g->clen - 1 && split_q > 0) {
+        /* supplementary: leading H (or S) for the clipped prefix, then the rest aligned */
+        if (rb_reserve_ops(b, 3ull * (uint64_t)split_q + 16)) return -1;
+        if (rb_begin(b, g->tid, split_ref, 0x800)) return -1;
+        rb_op(b, rng_unif(r) < 0.5 ? OP_H : OP_S, (uint32_t)(qlen - split_q > 0 ? qlen - split_q : 1));
+        int32_t ref2 = split_ref, q2 = split_q;
+        while (q2 > 0 && ref2 < g->clen - 1) {
+            int32_t m = rng_geom(r, mean_m);
+            if (m > q2) m = q2;
+            rb_op(b, OP_M, (uint32_t)m); ref2 += m; q2 -= m;
+            if (q2 <= 0) break;
+            small_event(g, &ref2, &q2);
+        }
+        if (b->nops == b->off[b->n] + 1) rb_op(b, OP_M, 1);
+        rb_end(b);
+    }
+    return 0;
+}
+
+/* htslib bam_endpos: pos + (unmapped ? 0 : sum of M/D/N/=/X lengths), 0 -> 1 */
+static int32_t endpos_of(int32_t pos, uint16_t flag, const uint32_t *ops, uint64_t n) {
+    int64_t rl = 0;
+    if (!(flag & 4))
+        for (uint64_t i = 0; i < n; i++) {
+            uint32_t op = ops[i] & 0xf;
+            if (op == OP_M || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X) rl += ops[i] >> 4;
+        }
+    if (rl == 0) rl = 1;
+    return (int32_t)(pos + rl);
+}
+
+static int cmp_locus(const void *a, const void *b) {
+    const locus_t *x = (const locus_t *)a, *y = (const locus_t *)b;
+    return (x->bp1 > y->bp1) - (x->bp1 < y->bp1);
+}
+
+typedef struct { int32_t pos; int32_t idx; } sortkey_t;
+static int cmp_key(const void *a, const void *b) {
+    const sortkey_t *x = (const sortkey_t *)a, *y = (const sortkey_t *)b;
+    if (x->pos != y->pos) return (x->pos > y->pos) - (x->pos < y->pos);
+    return (x->idx > y->idx) - (x->idx < y->idx);
+}
+
+sim_pileup *sim_generate(const sim_config *c) {
+    if (!c || c->n_targets < 1 || c->n_loci < 0) return NULL;
+    sim_pileup *p = (sim_pileup *)calloc(1, sizeof(sim_pileup));
+    if (!p) return NULL;
+    rng_t rng;
+    rng_seed(&rng, c->seed);
+    p->n_targets = c->n_targets;
+    p->n_loci = c->n_loci;
+    p->contig_len = (int32_t *)calloc((size_t)c->n_targets, sizeof(int32_t));
+    p->loci = (int32_t *)calloc((size_t)(c->n_loci > 0 ? c->n_loci : 1) * 4, sizeof(int32_t));
+    p->truth = (int32_t *)calloc((size_t)(c->n_loci > 0 ? c->n_loci : 1) * 2, sizeof(int32_t));
+    locus_t *L = (locus_t *)calloc((size_t)(c->n_loci > 0 ? c->n_loci : 1), sizeof(locus_t));
+    if (!p->contig_len || !p->loci || !p->truth || !L) { free(L); sim_free(p); return NULL; }
+
+    /* loci: contig-major, evenly spaced with random offsets */
+    int32_t per = (c->n_loci + c->n_targets - 1) / c->n_targets;
+    if (per < 1) per = 1;
+    for (int32_t t = 0; t < c->n_targets; t++)
+        p->contig_len[t] = c->first_offset + per * c->spacing + c->first_offset;
+    double lmin = log((double)c->sv_min_len), lmax = log((double)c->sv_max_len);
+    for (int32_t k = 0; k < c->n_loci; k++) {
+        int32_t t = k / per, slot = k % per;
+        int32_t base = c->first_offset + slot * c->spacing;
+        int32_t bp1 = base + rng_int(&rng, 0, c->spacing / 8);
+        int32_t len = (int32_t)floor(exp(lmin + (lmax - lmin) * rng_unif(&rng)));
+        if (len < c->sv_min_len) len = c->sv_min_len;
+        int32_t type = rng_unif(&rng) < c->del_frac ? 2 : 1;
+        int32_t bp2 = bp1 + len;
+        int32_t rj = c->report_jitter;
+        int32_t rpos = bp1 + (rj ? rng_int(&rng, -rj, rj) : 0);
+        int32_t rend = type == 2 ? bp2 + (rj ? rng_int(&rng, -rj, rj) : 0) : rpos + 1;
+        L[k] = (locus_t){type, t + 1, rpos, rend, bp1, bp2, t};
+        p->loci[4 * k + 0] = type; p->loci[4 * k + 1] = t + 1;
+        p->loci[4 * k + 2] = rpos; p->loci[4 * k + 3] = rend;
+        p->truth[2 * k + 0] = bp1; p->truth[2 * k + 1] = bp2;
+    }
+
+    rbuf b;
+    memset(&b, 0, sizeof b);
+    b.off = (uint64_t *)calloc(1, sizeof(uint64_t));
+    if (!b.off) { free(L); sim_free(p); return NULL; }
+    double mean_gap = (double)c->read_len_mean / (c->coverage > 0 ? c->coverage : 1.0);
+    for (int32_t t = 0; t < c->n_targets; t++) {
+        /* this contig's SVs, sorted by bp1 */
+        int32_t n0 = t * per, n1 = (t + 1) * per;
+        if (n1 > c->n_loci) n1 = c->n_loci;
+        if (n0 > n1) n0 = n1;
+        locus_t *sv = L + n0;
+        qsort(sv, (size_t)(n1 - n0), sizeof(locus_t), cmp_locus);
+        gen_t g = {c, &rng, &b, sv, n1 - n0, t, p->contig_len[t]};
+        int32_t cursor = 0;
+        double x = -(double)c->read_len_mean;   /* starts drift in from before 0 */
+        for (;;) {
+            double u = rng_unif(&rng);
+            if (u < 1e-300) u = 1e-300;
+            x += -log(u) * mean_gap;
+            if (x >= (double)(p->contig_len[t] - 1)) break;
+            int32_t qlen = (int32_t)(c->read_len_mean + c->read_len_sd * rng_norm(&rng));
+            if (qlen < c->read_len_min) qlen = c->read_len_min;
+            int32_t start = (int32_t)x;
+            if (start < 0) { qlen += start; start = 0; if (qlen < 1) continue; }
+            while (cursor < g.nsv && g.sv[cursor].bp2 + 2 * c->bp_jitter + 2 < start) cursor++;
+            if (make_read(&g, start, qlen, &cursor)) { free(L); free(b.pos); free(b.flag); free(b.off); free(b.tid); free(b.ops); sim_free(p); return NULL; }
+        }
+    }
+    free(L);
+
+    /* sort reads per contig by pos (supplementaries were appended out of order) */
+    p->n_reads = b.n;
+    p->n_ops = b.nops;
+    sortkey_t *keys = (sortkey_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(sortkey_t));
+    p->tid_off = (int64_t *)calloc((size_t)c->n_targets + 1, sizeof(int64_t));
+    p->pos = (int32_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(int32_t));
+    p->endpos = (int32_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(int32_t));
+    p->flag = (uint16_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(uint16_t));
+    p->cig_off = (uint64_t *)malloc((size_t)(b.n + 1) * sizeof(uint64_t));
+    p->cigar = (uint32_t *)malloc((size_t)(b.nops > 0 ? b.nops : 1) * sizeof(uint32_t));
+    if (!keys || !p->tid_off || !p->pos || !p->endpos || !p->flag || !p->cig_off || !p->cigar) {
+        free(keys); free(b.pos); free(b.flag); free(b.off); free(b.tid); free(b.ops); sim_free(p); return NULL;
+    }
+    int64_t w = 0;
+    uint64_t wo = 0;
+    int64_t r0 = 0;
+    for (int32_t t = 0; t < c->n_targets; t++) {
+        int64_t r1 = r0;
+        while (r1 < b.n && b.tid[r1] == t) r1++;
+        int64_t k = 0;
+        for (int64_t i = r0; i < r1; i++, k++) { keys[k].pos = b.pos[i]; keys[k].idx = (int32_t)(i - r0); }
+        qsort(keys, (size_t)k, sizeof(sortkey_t), cmp_key);
+        p->tid_off[t] = w;
+        for (int64_t i = 0; i < k; i++) {
+            int64_t s = r0 + keys[i].idx;
+            uint64_t n = b.off[s + 1] - b.off[s];
+            memcpy(p->cigar + wo, b.ops + b.off[s], n * sizeof(uint32_t));
+            p->pos[w] = b.pos[s];
+            p->flag[w] = b.flag[s];
+            p->cig_off[w] = wo;
+            p->endpos[w] = endpos_of(b.pos[s], b.flag[s], p->cigar + wo, n);
+            wo += n;
+            w++;
+        }
+        r0 = r1;
+    }
+    p->tid_off[c->n_targets] = w;
+    p->cig_off[w] = wo;
+    free(keys); free(b.pos); free(b.flag); free(b.off); free(b.tid); free(b.ops);
+    return p;
+}
+
+void sim_free(sim_pileup *p) {
+    if (!p) return;
+    free(p->contig_len); free(p->tid_off); free(p->pos); free(p->endpos); free(p->cig_off);
+    free(p->cigar); free(p->flag); free(p->loci); free(p->truth); free(p);
+}
+
+int32_t sim_n_targets(const sim_pileup *p) { return p->n_targets; }
+int32_t sim_contig_len(const sim_pileup *p, int32_t t) { return (t >= 0 && t < p->n_targets) ? p->contig_len[t] : 0; }
+int64_t sim_n_reads(const sim_pileup *p) { return p->n_reads; }
+uint64_t sim_n_ops(const sim_pileup *p) { return p->n_ops; }
+const int64_t *sim_tid_off(const sim_pileup *p) { return p->tid_off; }
+const int32_t *sim_pos(const sim_pileup *p) { return p->pos; }
+const int32_t *sim_endpos(const sim_pileup *p) { return p->endpos; }
+const uint64_t *sim_cig_off(const sim_pileup *p) { return p->cig_off; }
+const uint32_t *sim_cigar(const sim_pileup *p) { return p->cigar; }
+const uint16_t *sim_flag(const sim_pileup *p) { return p->flag; }
+int32_t sim_n_loci(const sim_pileup *p) { return p->n_loci; }
+const int32_t *sim_loci(const sim_pileup *p) { return p->loci; }
+const int32_t *sim_truth(const sim_pileup *p) { return p->truth; }
+
+/* ---------------------------------------------------------------- BAM writer */
+typedef struct {
+    FILE *f;
+    uint8_t buf[65280];
+    size_t n;
+    int level;
+    int err;
+} bgzf_w;
+
+static void bgzf_flush(bgzf_w *w) {
+    if (w->err) return;
+    uint8_t out[65536];
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, w->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { w->err = 1; return; }
+    zs.next_in = w->buf; zs.avail_in = (uInt)w->n;
+    zs.next_out = out + 18; zs.avail_out = (uInt)(sizeof(out) - 26);
+    if (deflate(&zs, Z_FINISH) != Z_STREAM_END) { deflateEnd(&zs); w->err = 1; return; }
+    size_t clen = zs.total_out;
+    deflateEnd(&zs);
+    size_t bsize = clen + 26;   /* whole block */
+    static const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
+    memcpy(out, hdr, 16);
+    out[16] = (uint8_t)((bsize - 1) & 0xff);
+    out[17] = (uint8_t)((bsize - 1) >> 8);
+    uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), w->buf, (uInt)w->n);
+    uint8_t *t = out + 18 + clen;
+    t[0] = crc & 0xff; t[1] = (crc >> 8) & 0xff; t[2] = (crc >> 16) & 0xff; t[3] = crc >> 24;
+    uint32_t isz = (uint32_t)w->n;
+    t[4] = isz & 0xff; t[5] = (isz >> 8) & 0xff; t[6] = (isz >> 16) & 0xff; t[7] = isz >> 24;
+    if (fwrite(out, 1, bsize, w->f) != bsize) w->err = 1;
+    w->n = 0;
+}
+static void bgzf_put(bgzf_w *w, const void *data, size_t len) {
+    const uint8_t *d = (const uint8_t *)data;
+    while (len) {
+        size_t k = sizeof(w->buf) - w->n;
+        if (k > len) k = len;
+        memcpy(w->buf + w->n, d, k);
+        w->n += k; d += k; len -= k;
+        if (w->n == sizeof(w->buf)) bgzf_flush(w);
+    }
+}
+static void put32(bgzf_w *w, int32_t v) { uint8_t b[4] = {(uint8_t)v, (uint8_t)(v >> 8), (uint8_t)(v >> 16), (uint8_t)(v >> 24)}; bgzf_put(w, b, 4); }
+
+/* SAM spec reg2bin for [beg, end) */
+static int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level) {
+    bgzf_w *w = (bgzf_w *)calloc(1, sizeof(bgzf_w));
+    if (!w) return -1;
+    w->f = fopen(path, "wb");
+    if (!w->f) { free(w); return -1; }
+    w->level = level < 0 ? 6 : level;
+    rng_t rng;
+    rng_seed(&rng, 0x5eed5eedull);
+    /* header */
+    char text[4096];
+    int tl = snprintf(text, sizeof text, "@HD\tVN:1.6\tSO:coordinate\n");
+    bgzf_put(w, "BAM\1", 4);
+    /* @SQ lines can exceed the buffer for many contigs; emit them piecewise */
+    size_t sq_len = 0;
+    for (int t = 0; t < p->n_targets; t++) {
+        char line[128];
+        sq_len += (size_t)snprintf(line, sizeof line, "@SQ\tSN:%d\tLN:%d\n", t + 1, p->contig_len[t]);
+    }
+    put32(w, (int32_t)((size_t)tl + sq_len));
+    bgzf_put(w, text, (size_t)tl);
+    for (int t = 0; t < p->n_targets; t++) {
+        char line[128];
+        int k = snprintf(line, sizeof line, "@SQ\tSN:%d\tLN:%d\n", t + 1, p->contig_len[t]);
+        bgzf_put(w, line, (size_t)k);
+    }
+    put32(w, p->n_targets);
+    for (int t = 0; t < p->n_targets; t++) {
+        char name[32];
+        int k = snprintf(name, sizeof name, "%d", t + 1);
+        put32(w, k + 1);
+        bgzf_put(w, name, (size_t)k + 1);
+        put32(w, p->contig_len[t]);
+    }
+    /* records */
+    uint8_t *rec = NULL;
+    size_t rec_cap = 0;
+    static const char nt16[] = "=ACMGRSVTWYHKDBN";
+    for (int t = 0; t < p->n_targets; t++) {
+        for (int64_t r = p->tid_off[t]; r < p->tid_off[t + 1]; r++) {
+            const uint32_t *ops = p->cigar + p->cig_off[r];
+            uint64_t n = p->cig_off[r + 1] - p->cig_off[r];
+            int64_t qlen = 0, rlen = 0;
+            for (uint64_t i = 0; i < n; i++) {
+                uint32_t op = ops[i] & 0xf, l = ops[i] >> 4;
+                if (op == OP_M || op == OP_I || op == OP_S || op == OP_EQ || op == OP_X) qlen += l;
+                if (op == OP_M || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X) rlen += l;
+            }
+            int32_t l_seq = with_seq ? (int32_t)qlen : 0;
+            char qname[32];
+            int lq = snprintf(qname, sizeof qname, "r%lld", (long long)r) + 1;
+            int use_cg = n > 65535;
+            uint32_t n_cig_field = use_cg ? 2u : (uint32_t)n;
+            size_t need = 32 + (size_t)lq + 4 * (size_t)n_cig_field + (size_t)(l_seq + 1) / 2 + (size_t)l_seq +
+                          (use_cg ? 8 + 4 * n : 0);
+            if (need > rec_cap) {
+                rec_cap = need * 2;
+                uint8_t *x = (uint8_t *)realloc(rec, rec_cap);
+                if (!x) { free(rec); fclose(w->f); free(w); return -1; }
+                rec = x;
+            }
+            uint8_t *q = rec + 4;
+            int32_t hdr32[8];
+            hdr32[0] = t;
+            hdr32[1] = p->pos[r];
+            hdr32[2] = (int32_t)((uint32_t)reg2bin(p->pos[r], p->endpos[r]) << 16 | (uint32_t)60 << 8 | (uint32_t)lq);
+            hdr32[3] = (int32_t)((uint32_t)p->flag[r] << 16 | n_cig_field);
+            hdr32[4] = l_seq;
+            hdr32[5] = -1; hdr32[6] = -1; hdr32[7] = 0;
+            memcpy(q, hdr32, 32); q += 32;
+            memcpy(q, qname, (size_t)lq); q += lq;
+            if (use_cg) {
+                uint32_t fake[2] = {(uint32_t)l_seq << 4 | OP_S, (uint32_t)rlen << 4 | OP_N};
+                memcpy(q, fake, 8); q += 8;
+            } else {
+                memcpy(q, ops, 4 * n); q += 4 * n;
+            }
+            for (int32_t i = 0; i < (l_seq + 1) / 2; i++) {
+                uint8_t a = (uint8_t)(1u << (rng_u64(&rng) & 3)), c2 = (uint8_t)(1u << (rng_u64(&rng) & 3));
+                (void)nt16;
+                *q++ = (uint8_t)(a << 4 | c2);
+            }
+            for (int32_t i = 0; i < l_seq; i++) *q++ = (uint8_t)(10 + (rng_u64(&rng) % 30));
+            if (use_cg) {
+                q[0] = 'C'; q[1] = 'G'; q[2] = 'B'; q[3] = 'I';
+                uint32_t cnt = (uint32_t)n;
+                memcpy(q + 4, &cnt, 4);
+                memcpy(q + 8, ops, 4 * n);
+                q += 8 + 4 * n;
+            }
+            int32_t bs = (int32_t)(q - rec - 4);
+            memcpy(rec, &bs, 4);
+            bgzf_put(w, rec, (size_t)(q - rec));
+        }
+    }
+    free(rec);
+    if (w->n) bgzf_flush(w);
+    static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (!w->err && fwrite(eof, 1, 28, w->f) != 28) w->err = 1;
+    int err = w->err;
+    if (fclose(w->f)) err = 1;
+    free(w);
+    return err ? -1 : 0;
+}

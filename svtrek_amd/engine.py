@@ -1,0 +1,117 @@
+"""Python host mirror of the reference's per-record refinement calls, over the C ABI.
+
+`Engine.refine(loci)` is the batched form of what thread_func (reference
+audit.c:175-232) does per record through deletion()/insertion()/inversion()
+(refinement.c:327-339): same parameters (t_arg's six refinement fields,
+params.h:81-87, defaults params.h:27-32), same result encoding (0xFFFFFFFF = the
+reference's -1 "not refined").  Every call runs the HIP engine; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import (LOCUS_DTYPE, RESULT_DTYPE, STATUS_NAMES, SvtParams, SvtWork, load_engine, ptr)
+from .pileup import Pileup
+
+# params.h:27-32
+WIDER_INTERVAL = 20000
+MEDIAN_INTERVAL = 10000
+NARROW_INTERVAL = 2000
+CONSENSUS_INTERVAL_RANGE = 500
+CONSENSUS_INTERVAL = 5
+CONSENSUS_MIN_COUNT = 3
+
+
+@dataclass
+class Params:
+    wider_interval: int = WIDER_INTERVAL
+    median_interval: int = MEDIAN_INTERVAL
+    narrow_interval: int = NARROW_INTERVAL
+    consensus_interval_range: int = CONSENSUS_INTERVAL_RANGE
+    consensus_interval: int = CONSENSUS_INTERVAL
+    consensus_min_count: int = CONSENSUS_MIN_COUNT
+    spill_bytes: int = 0
+
+    def to_c(self) -> SvtParams:
+        return SvtParams(self.wider_interval, self.median_interval, self.narrow_interval,
+                         self.consensus_interval_range, self.consensus_interval, self.consensus_min_count,
+                         self.spill_bytes)
+
+
+class SvtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"svt error {code} ({STATUS_NAMES.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Engine:
+    """One GPU context (svt_ctx).  Use one Engine per process/GPU."""
+
+    def __init__(self, params: Params | None = None, device: int = -1):
+        self.lib = load_engine()
+        self.params = params or Params()
+        self._cp = self.params.to_c()
+        h = C.c_void_p()
+        rc = self.lib.svt_open(C.byref(self._cp), int(device), C.byref(h))
+        if rc != 0:
+            raise SvtError(rc, "svt_open failed (no HIP device, or consensus_min_count < 1)")
+        self._h = h
+        self._pileup = None
+
+    def _check(self, rc: int) -> None:
+        if rc != 0:
+            raise SvtError(rc, self.lib.svt_last_error(self._h).decode(errors="replace"))
+
+    def load_pileup(self, pileup: Pileup) -> None:
+        view = pileup.view()
+        self._check(self.lib.svt_load_pileup(self._h, C.byref(view)))
+        self._pileup = pileup
+
+    def refine(self, loci: np.ndarray) -> np.ndarray:
+        loci = np.ascontiguousarray(loci, dtype=LOCUS_DTYPE)
+        out = np.empty(len(loci), dtype=RESULT_DTYPE)
+        if len(loci):
+            self._check(self.lib.svt_refine_batch(self._h, ptr(loci), len(loci), ptr(out)))
+        return out
+
+    def refine_device(self, d_loci: int, n: int, d_out: int, stream: int | None = None) -> None:
+        """Device pointers (e.g. torch tensor .data_ptr()) on a hipStream_t handle (int)."""
+        self._check(self.lib.svt_refine_device(self._h, C.c_void_p(d_loci), n, C.c_void_p(d_out),
+                                               C.c_void_p(stream or 0)))
+
+    def sync(self, stream: int | None = None) -> None:
+        self._check(self.lib.svt_sync(self._h, C.c_void_p(stream or 0)))
+
+    def count_work(self, loci: np.ndarray) -> dict:
+        loci = np.ascontiguousarray(loci, dtype=LOCUS_DTYPE)
+        w = SvtWork()
+        self._check(self.lib.svt_count_work(self._h, ptr(loci), len(loci), C.byref(w)))
+        return {f: int(getattr(w, f)) for f, _ in SvtWork._fields_}
+
+    @property
+    def device_bytes(self) -> int:
+        return int(self.lib.svt_pileup_device_bytes(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.svt_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def version() -> str:
+    return load_engine().svt_version().decode()

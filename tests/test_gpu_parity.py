@@ -1,0 +1,198 @@
+"""HIP engine vs CPU oracle: bit-exact refined breakpoints (integer path, no tolerance).
+
+All calls go through the C ABI (libsvtrek_hip.so via svtrek_amd.Engine).
+"""
+import numpy as np
+import oracle_ffi as O
+import pytest
+
+from svtrek_amd import SVT_NA, Engine, Params, make_loci, sim
+from svtrek_amd._lib import LOCUS_DTYPE
+
+from fuzz import cluster_pileup, random_loci, random_pileup
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(got, want, loci):
+    bad = np.nonzero((got["start"] != want["start"]) | (got["end"] != want["end"]))[0]
+    if len(bad):
+        i = int(bad[0])
+        raise AssertionError(f"{len(bad)} of {len(loci)} loci differ; first #{i} locus={loci[i]} "
+                             f"gpu={got[i]} oracle={want[i]}")
+
+
+def test_consensus_vectors_through_kernel(engine_factory):
+    """SURVEY A10 vectors routed through a DEL-start window of a synthetic pileup."""
+    from test_oracle_consensus import SURVEY_VECTORS
+    eng = engine_factory()
+    base = 100000
+    for locs, pos, want in SURVEY_VECTORS:
+        vals = [base + v for v in locs]
+        pl = cluster_pileup(vals)
+        eng.load_pileup(pl)
+        loci = make_loci([(2, 1, base + pos, base + pos + 5000)])
+        got = eng.refine(loci)
+        exp = SVT_NA if want == -1 else base + want
+        assert int(got["start"][0]) == exp, (locs, pos, want, int(got["start"][0]))
+        assert int(O.refine_batch(pl, loci)["start"][0]) == exp
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_consensus_windows(engine_factory, seed):
+    rng = np.random.default_rng(seed)
+    eng = engine_factory(Params(consensus_interval=int(rng.choice([0, 1, 5, 12])),
+                                consensus_interval_range=int(rng.choice([50, 500, 900])),
+                                consensus_min_count=int(rng.choice([1, 2, 3, 5]))))
+    base = 200000
+    rows, vals = [], []
+    for k in range(40):
+        c = base + k * 60000
+        n = int(rng.integers(0, 40))
+        centers = c + rng.integers(-400, 400, size=3)
+        v = [int(rng.choice(centers)) + int(rng.integers(-8, 9)) for _ in range(n)]
+        vals.extend(v)
+        rows.append((2, 1, c + int(rng.integers(-30, 30)), c + 20000))
+    pl = cluster_pileup(vals)
+    eng.load_pileup(pl)
+    loci = make_loci(rows)
+    got = eng.refine(loci)
+    want = O.refine_batch(pl, loci, eng.params)
+    _assert_same(got, want, loci)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_fuzz_pileups(engine_factory, seed):
+    rng = np.random.default_rng(1000 + seed)
+    hot = [int(x) for x in rng.integers(5000, 55000, size=6)]
+    pl = random_pileup(rng, n_targets=2, contig_len=60000, n_reads=int(rng.integers(50, 700)),
+                       max_ops=int(rng.choice([3, 40, 150, 400])), hot=hot)
+    prm = Params(wider_interval=int(rng.choice([20000, 3000])), median_interval=int(rng.choice([10000, 500])),
+                 narrow_interval=int(rng.choice([2000, 100])), consensus_interval_range=int(rng.choice([500, 80])),
+                 consensus_interval=int(rng.choice([5, 0, 30])), consensus_min_count=int(rng.choice([1, 2, 3])))
+    eng = engine_factory(prm)
+    eng.load_pileup(pl)
+    loci = random_loci(rng, 300, 2, 60000, hot)
+    got = eng.refine(loci)
+    want = O.refine_batch(pl, loci, prm)
+    _assert_same(got, want, loci)
+
+
+def test_spill_path(engine_factory):
+    """> SVT_LDS_CANDS candidates in one window: the device spill pool keeps it exact."""
+    rng = np.random.default_rng(7)
+    base = 300000
+    vals = [base + int(x) for x in rng.integers(-300, 300, size=1500)] + [base + 3] * 40
+    pl = cluster_pileup(vals)
+    eng = engine_factory()
+    eng.load_pileup(pl)
+    loci = make_loci([(2, 1, base, base + 10000), (2, 1, base + 150, base + 9000), (1, 1, base, base)])
+    w = eng.count_work(loci)
+    assert w["spilled_windows"] >= 2
+    got = eng.refine(loci)
+    want = O.refine_batch(pl, loci)
+    _assert_same(got, want, loci)
+
+
+def test_spill_pool_exhaustion_reported(engine_factory):
+    vals = [400000 + i % 700 for i in range(3000)]
+    pl = cluster_pileup(vals)
+    eng = engine_factory(Params(spill_bytes=1024))
+    eng.load_pileup(pl)
+    from svtrek_amd import SvtError
+    with pytest.raises(SvtError):
+        eng.refine(make_loci([(2, 1, 400100, 410000)]))
+
+
+def test_long_cigars(engine_factory):
+    """Reads with thousands of ops (multi-chunk scans, break deep inside a chunk)."""
+    rng = np.random.default_rng(3)
+    rows = []
+    for k in range(120):
+        pos = int(rng.integers(0, 20000))
+        ops = []
+        for j in range(int(rng.integers(500, 5000))):
+            ops.append((int(rng.choice([0, 0, 1, 2, 8])), int(rng.integers(1, 9))))
+        if rng.random() < 0.6:
+            cut = int(rng.integers(0, len(ops)))
+            ops.insert(cut, (2, int(rng.choice([51, 300]))))
+        rows.append((0, pos, ops))
+    from svtrek_amd.pileup import from_reads
+    pl = from_reads(1, rows)
+    eng = engine_factory()
+    eng.load_pileup(pl)
+    loci = make_loci([(2, 1, int(p), int(p) + int(e)) for p, e in
+                      zip(rng.integers(0, 40000, 200), rng.integers(51, 20000, 200))] +
+                     [(1, 1, int(p), int(p) + 1) for p in rng.integers(0, 40000, 100)])
+    got = eng.refine(loci)
+    want = O.refine_batch(pl, loci)
+    _assert_same(got, want, loci)
+
+
+def test_inv_and_unknown_types(engine_factory):
+    pl = cluster_pileup([10000] * 10)
+    eng = engine_factory()
+    eng.load_pileup(pl)
+    loci = make_loci([(3, 1, 10000, 20000), (4, 1, 10000, 20000), (0, 1, 10000, 10100)])
+    got = eng.refine(loci)
+    assert (got["start"] == SVT_NA).all() and (got["end"] == SVT_NA).all()
+    want = O.refine_batch(pl, loci)
+    _assert_same(got, want, loci)
+
+
+def test_empty_inputs(engine_factory):
+    from svtrek_amd.pileup import from_reads
+    eng = engine_factory()
+    eng.load_pileup(from_reads(3, []))
+    assert len(eng.refine(np.zeros(0, dtype=LOCUS_DTYPE))) == 0
+    loci = make_loci([(2, 1, 100000, 101000), (1, 3, 5, 6)])
+    got = eng.refine(loci)
+    assert (got["start"] == SVT_NA).all() and (got["end"] == SVT_NA).all()
+
+
+@pytest.mark.parametrize("name", ["cfg1_100del_10x"])
+def test_workload_cfg1_full(engine_factory, name):
+    r = sim.generate(sim.WORKLOADS[name])
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    got = eng.refine(r.loci)
+    want = O.refine_batch(r.pileup, r.loci)
+    _assert_same(got, want, r.loci)
+    assert (got["start"] != SVT_NA).mean() > 0.5
+
+
+def test_workload_exotic_ops(engine_factory):
+    cfg = sim.SimConfig(seed=9, n_targets=2, n_loci=400, del_frac=0.5, coverage=20, p_exotic=0.05,
+                        p_clip_ends=0.3, p_noise_sv=0.3)
+    r = sim.generate(cfg)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    got = eng.refine(r.loci)
+    want = O.refine_batch(r.pileup, r.loci, threads=4)
+    _assert_same(got, want, r.loci)
+
+
+def test_workload_cfg2_full_parity(engine_factory):
+    """BASELINE config 2 at full size (10k DEL, 30x ONT-like): every locus bit-exact."""
+    r = sim.generate(sim.WORKLOADS["cfg2_10kdel_30x_ont"])
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    got = eng.refine(r.loci)
+    want, ow = O.refine_batch(r.pileup, r.loci, threads=8, with_work=True)
+    _assert_same(got, want, r.loci)
+    w = eng.count_work(r.loci)
+    assert (w["windows"], w["reads"], w["ops_walked"], w["candidates"]) == \
+        (ow["windows"], ow["reads"], ow["ops_walked"], ow["candidates"])
+
+
+def test_repeatability_and_batch_split(engine_factory):
+    """Order/batching independence (loci are independent, audit.c:50-248)."""
+    r = sim.generate(sim.SimConfig(seed=77, n_loci=500, n_targets=2, del_frac=0.6))
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    a = eng.refine(r.loci)
+    perm = np.random.default_rng(0).permutation(len(r.loci))
+    b = eng.refine(r.loci[perm])
+    assert (b == a[perm]).all()
+    c = np.concatenate([eng.refine(r.loci[:123]), eng.refine(r.loci[123:])])
+    assert (c == a).all()
