@@ -1,0 +1,225 @@
+// svtrek_main.cpp -- `svtrek audt -b BAM -v VCF [OPTIONS]`, drop-in for the reference CLI
+// (svtrek.c:5-22, init.c:21-147, audit.c:250-368) on MI355X.
+//
+// Same flags, defaults and stdout bytes as the reference; records are printed in VCF
+// order (the reference prints in worker completion order and drops up to 2*T trailing
+// records through its exit_signal race, SURVEY.md §3.1 -- not reproduced).  The work
+// between the two [INFO] lines is: read the BAM once into a columnar pileup (host,
+// -t inflate threads), copy it to HBM, parse all VCF records (A1), refine them in
+// batched HIP launches (svt_refine_batch; --gpus N shards records over N devices,
+// one host thread and one svt_ctx per device), print (A11).
+#include <getopt.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "svtrek_gpu.h"
+#include "svtrek_host.h"
+
+namespace {
+
+// params.h:27-36
+constexpr int WIDER = 20000, MEDIAN = 10000, NARROW = 2000, CI_RANGE = 500, CI = 5, MIN_COUNT = 3, THREADS = 4;
+
+void usage() {
+    printf("Usage: ./svtrek [MODE] [OPTIONS]\n");
+    printf("Mode:\n");
+    printf("    disc    Variation discovery on graph alignment result.\n");
+    printf("    audt    Audit the reported variations on VCF using BAM.\n");
+}
+
+void audt_usage() {
+    printf("Usage: ./svtrek audt [-b|--bam BAM] [-v|--vcf VCF file] [OPTIONS]\n");
+    printf("Options:\n");
+    printf("    [-o|--ouput] <filename>           Output filename [Default: svtrek.out]\n");
+    printf("    -t <num>                          Thread number [Default: %d]\n", THREADS);
+    printf("    --verbose                         Verbose [Default: false]\n\n");
+    printf("    --wider-interval <num>            Interval for the offset of the reads to start [Default: %d]\n", WIDER);
+    printf("    --median-interval <num>           Interval for the offset of the reads (for point) [Default: %d]\n", MEDIAN);
+    printf("    --narrow-interval <num>           Interval for the offset of the reads to end [Default: %d]\n", NARROW);
+    printf("    --consensus-interval-range <num>  The interval to limit refinement range [DEFAULT: %d]\n", CI_RANGE);
+    printf("    --consensus-interval <num>        The interval that is considered into the same position [DEFAULT: %d]\n", CI);
+    printf("    --consensus-min-count <num>       Minimum number of elements needs for the consensus [Default: %d]\n\n", MIN_COUNT);
+    printf("GPU options (svtrek_amd):\n");
+    printf("    --gpus <num>                      GPUs to shard records over [Default: 1]\n");
+    printf("    --device <num>                    First GPU index [Default: 0]\n");
+    printf("    --batch <num>                     Records per GPU launch [Default: 1048576]\n");
+}
+
+struct Args {
+    const char *bam = nullptr, *vcf = nullptr, *out = "svtrek.out";
+    int threads = THREADS, verbose = 0, gpus = 1, device = 0;
+    size_t batch = 1u << 20;
+    svt_params prm{WIDER, MEDIAN, NARROW, CI_RANGE, CI, MIN_COUNT, 0};
+};
+
+void validate_file(const char *f, const char *msg) {   // init.c:35-47 (without its fclose(NULL) crash)
+    if (!f) {
+        fprintf(stderr, "%s\n", msg);
+        exit(EXIT_FAILURE);
+    }
+    FILE *fp = fopen(f, "r");
+    if (!fp) {
+        fprintf(stderr, "[ERROR]: File couldn't be opened %s\n", f);
+        exit(EXIT_FAILURE);
+    }
+    fclose(fp);
+}
+
+Args parse_audt(int argc, char **argv) {
+    Args a;
+    if (argc < 2) {
+        audt_usage();
+        exit(1);
+    }
+    static const option opts[] = {
+        {"bam", required_argument, nullptr, 1}, {"vcf", required_argument, nullptr, 2},
+        {"output", required_argument, nullptr, 3}, {"verbose", no_argument, nullptr, 4},
+        {"wider-interval", required_argument, nullptr, 5}, {"median-interval", required_argument, nullptr, 6},
+        {"narrow-interval", required_argument, nullptr, 7},
+        {"consensus-interval-range", required_argument, nullptr, 8},
+        {"consensus-interval", required_argument, nullptr, 9},
+        {"consensus-min-count", required_argument, nullptr, 10}, {"help", no_argument, nullptr, 11},
+        {"gpus", required_argument, nullptr, 20}, {"device", required_argument, nullptr, 21},
+        {"batch", required_argument, nullptr, 22}, {nullptr, 0, nullptr, 0}};
+    int opt, li;
+    while ((opt = getopt_long(argc, argv, "b:v:o:t:h", opts, &li)) != -1) {
+        switch (opt) {
+        case 'b': case 1: a.bam = optarg; break;
+        case 'v': case 2: a.vcf = optarg; break;
+        case 'o': case 3: a.out = optarg; break;   // parsed, unused (as in the reference)
+        case 4: a.verbose = 1; break;
+        case 't': a.threads = atoi(optarg); break;
+        case 5: a.prm.wider_interval = atoi(optarg); break;
+        case 6: a.prm.median_interval = atoi(optarg); break;
+        case 7: a.prm.narrow_interval = atoi(optarg); break;
+        case 8: a.prm.consensus_interval_range = atoi(optarg); break;
+        case 9: a.prm.consensus_interval = atoi(optarg); break;
+        case 10: a.prm.consensus_min_count = atoi(optarg); break;
+        case 'h': case 11: audt_usage(); exit(EXIT_SUCCESS);
+        case 20: a.gpus = atoi(optarg); break;
+        case 21: a.device = atoi(optarg); break;
+        case 22: a.batch = (size_t)strtoull(optarg, nullptr, 10); break;
+        default:
+            printf("[ERROR] Option %d is invalid.\n", opt);
+            audt_usage();
+            exit(EXIT_FAILURE);
+        }
+    }
+    validate_file(a.bam, "[ERROR] BAM file is not provided.");
+    validate_file(a.vcf, "[ERROR] VCF file is not provided.");
+    // The reference deadlocks on -t 0 and reads locations[-1] for min-count <= 0.
+    if (a.threads < 1) { fprintf(stderr, "[ERROR] -t must be >= 1\n"); exit(EXIT_FAILURE); }
+    if (a.prm.consensus_min_count < 1) { fprintf(stderr, "[ERROR] --consensus-min-count must be >= 1\n"); exit(EXIT_FAILURE); }
+    if (a.gpus < 1) a.gpus = 1;
+    if (a.batch < 1) a.batch = 1;
+    return a;
+}
+
+bool read_file(const char *path, std::string &s) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return false;
+    char buf[1 << 16];
+    size_t k;
+    while ((k = fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, k);
+    fclose(f);
+    return true;
+}
+
+int audit(int argc, char **argv) {
+    Args a = parse_audt(argc, argv);
+    printf("[INFO] Started processing variation file.\n");
+    fflush(stdout);
+
+    char err[512];
+    svth_bam *bam = svth_bam_read(a.bam, a.threads, err, sizeof err);
+    if (!bam) { fprintf(stderr, "[ERROR] %s\n", err); return 1; }
+    svt_pileup_view view;
+    svth_bam_view(bam, &view);
+
+    std::string vcf;
+    if (!read_file(a.vcf, vcf)) { fprintf(stderr, "[ERROR]: File couldn't be opened %s\n", a.vcf); return 1; }
+
+    // A1 over every data line (process_vcf's reader loop, audit.c:301-338)
+    std::vector<svt_locus> loci;
+    std::vector<std::string> line_buf;
+    std::string line;
+    size_t i = 0;
+    while (i < vcf.size()) {
+        size_t j = vcf.find('\n', i);
+        size_t len = (j == std::string::npos ? vcf.size() : j + 1) - i;
+        line.assign(vcf, i, len);
+        i += len;
+        if (len < 2 || line[0] == '#') continue;
+        if (line.back() == '\n') line.pop_back();
+        svt_locus l;
+        char perr[1024];
+        int act = svth_parse_line(&line[0], &l, perr, sizeof perr);
+        if (act == 2) fputs(perr, stderr);
+        if (act != 1) continue;
+        if (svth_is_unknown_type(&l)) fprintf(stderr, "[ERROR] Unkown type.\n");
+        loci.push_back(l);
+    }
+
+    std::vector<svt_result> res(loci.size());
+    const int G = a.gpus;
+    std::vector<int> rc(G, 0);
+    std::vector<std::string> gerr(G);
+    auto worker = [&](int g) {
+        size_t n = loci.size(), per = (n + G - 1) / G;
+        size_t b0 = std::min(n, per * (size_t)g), b1 = std::min(n, b0 + per);
+        svt_ctx *ctx = nullptr;
+        int s = svt_open(&a.prm, a.device + g, &ctx);
+        if (s) { rc[g] = s; gerr[g] = "svt_open failed (HIP device?)"; return; }
+        s = svt_load_pileup(ctx, &view);
+        for (size_t k = b0; !s && k < b1; k += a.batch) {
+            size_t m = std::min(a.batch, b1 - k);
+            s = svt_refine_batch(ctx, loci.data() + k, m, res.data() + k);
+        }
+        if (s) { rc[g] = s; gerr[g] = svt_last_error(ctx); }
+        svt_close(ctx);
+    };
+    if (G == 1) worker(0);
+    else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; g++) th.emplace_back(worker, g);
+        for (auto &t : th) t.join();
+    }
+    for (int g = 0; g < G; g++)
+        if (rc[g]) { fprintf(stderr, "[ERROR] GPU %d: %s (status %d)\n", a.device + g, gerr[g].c_str(), rc[g]); return 1; }
+    svth_bam_free(bam);
+
+    // A11, in VCF order
+    std::string out;
+    out.reserve(loci.size() * 120);
+    char buf[512];
+    for (size_t k = 0; k < loci.size(); k++) {
+        int n = svth_format(&loci[k], &res[k], buf, sizeof buf);
+        if (n > 0) out.append(buf, (size_t)n);
+    }
+    fwrite(out.data(), 1, out.size(), stdout);
+    printf("[INFO] Ended processing variation file\n");
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        usage();
+        exit(1);
+    }
+    if (strcmp(argv[1], "audt") == 0) {
+        return audit(argc, argv);   // 0 on success; 1 on ingest/GPU errors (the reference crashes)
+    }
+    if (strcmp(argv[1], "disc") == 0) {
+        fprintf(stderr, "[ERROR] disc mode is not part of svtrek_amd (it implements the audt path only)\n");
+        return 1;
+    }
+    usage();
+    exit(1);
+}

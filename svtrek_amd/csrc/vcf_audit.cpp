@@ -1,0 +1,139 @@
+// vcf_audit.cpp -- VCF record parsing (A1) and refined-call printing (A11) for the
+// `svtrek audt` drop-in.  Behaviour follows the reference byte for byte:
+//   parse:  thread_func, reference audit.c:62-173 (strtok_r tokenisation, strstr
+//           "SVTYPE=" / "END=" -- the latter also matching inside "CIEND=" --, strtol
+//           into uint32, the length inference when SVTYPE is absent, the 50-bp filter);
+//   print:  audit.c:176-232 printf formats (%u / %d of uint32 values, NA for 0xFFFFFFFF).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "svtrek_host.h"
+
+namespace {
+
+constexpr int SV_MIN_LENGTH = 50;   // params.h:33
+
+int sv_type_of(const char *s) {     // parse_sv_type, audit.c:3-11
+    if (!strcmp(s, "INS") || !strcmp(s, "INS:ME")) return SVT_INS;
+    if (!strcmp(s, "DEL") || !strcmp(s, "DEL:ME")) return SVT_DEL;
+    if (!strcmp(s, "INV")) return SVT_INV;
+    if (!strcmp(s, "DUP")) return SVT_DUP;
+    if (!strcmp(s, "TRA")) return SVT_TRA;
+    if (!strcmp(s, "BND")) return SVT_BND;
+    return SVT_UNKNOWN;
+}
+
+// copy the value after `key` up to ';' (at most cap-1 bytes), as audit.c:119-129 / :148-158
+void info_value(const char *v, char *buf, size_t cap) {
+    const char *e = strchr(v, ';');
+    size_t len = e ? (size_t)(e - v) : strlen(v);
+    if (len >= cap) len = cap - 1;
+    memcpy(buf, v, len);
+    buf[len] = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int svth_parse_line(char *line, svt_locus *l, char *err, size_t errcap) {
+    char *save = nullptr, *alt_save = nullptr;
+    if (err && errcap) err[0] = 0;
+    char *chrom = strtok_r(line, "\t", &save);
+    char *index = strtok_r(nullptr, "\t", &save);
+    if (!index) {
+        if (err) snprintf(err, errcap, "VCF: no index at line: %s\n", line);
+        return 2;
+    }
+    strtok_r(nullptr, "\t", &save);                       // ID
+    char *seq = strtok_r(nullptr, "\t", &save);           // REF
+    char *alt = seq ? strtok_r(nullptr, "\t", &save) : nullptr;
+    if (!seq || !alt) {   // the reference dereferences NULL here; report and skip instead
+        if (err) snprintf(err, errcap, "VCF: truncated record at POS %s\n", index);
+        return 2;
+    }
+    size_t seq_len = strlen(seq), max_alt = 0, min_alt = 0x7FFFFFFF;
+    for (char *t = strtok_r(alt, ",", &alt_save); t; t = strtok_r(nullptr, ",", &alt_save)) {
+        size_t k = strlen(t);
+        if (k > max_alt) max_alt = k;
+        if (k < min_alt) min_alt = k;
+    }
+    strtok_r(nullptr, "\t", &save);                       // QUAL
+    strtok_r(nullptr, "\t", &save);                       // FILTER
+    char *info = strtok_r(nullptr, "\t", &save);          // INFO
+    if (!info) {
+        if (err) snprintf(err, errcap, "VCF: truncated record at POS %s\n", index);
+        return 2;
+    }
+    int chrom_index = strncmp(chrom, "chr", 3) == 0 ? atoi(chrom + 3) : atoi(chrom);
+    uint32_t pos = (uint32_t)strtol(index, nullptr, 10);
+    if (pos == 0 && index[0] != '0') {
+        if (err) snprintf(err, errcap, "[ERROR] Conversion error to pos %s\n", index);
+        return 2;
+    }
+    int type;
+    if (const char *sv = strstr(info, "SVTYPE=")) {
+        char b[16];
+        info_value(sv + 7, b, sizeof b);
+        type = sv_type_of(b);
+    } else if (seq_len == 1 && (size_t)SV_MIN_LENGTH < max_alt) {
+        type = SVT_INS;
+    } else if ((size_t)SV_MIN_LENGTH < seq_len && min_alt == 1) {
+        type = SVT_DEL;
+    } else {
+        return 0;
+    }
+    uint32_t end;
+    if (const char *es = strstr(info, "END=")) {
+        char b[32];
+        info_value(es + 4, b, sizeof b);
+        end = (uint32_t)strtol(b, nullptr, 10);
+        if (end == 0 && b[0] != '0') return 0;
+    } else {
+        end = pos + (uint32_t)seq_len;
+    }
+    if ((type == SVT_DEL || type == SVT_INV) && end - pos < (uint32_t)SV_MIN_LENGTH) return 0;
+    l->type = type;
+    l->chrom = chrom_index;
+    l->pos = pos;
+    l->end = end;
+    return 1;
+}
+
+int svth_is_unknown_type(const svt_locus *l) {
+    return !(l->type == SVT_INS || l->type == SVT_DEL || l->type == SVT_INV);
+}
+
+int svth_format(const svt_locus *l, const svt_result *r, char *buf, size_t cap) {
+    const uint32_t pos = l->pos, end = l->end;
+    buf[0] = 0;
+    if (l->type == SVT_INS) {
+        if (r->start == SVT_NA)
+            return snprintf(buf, cap, "(INS) chr: %d, org pos: %u, ref pos: NA\n", l->chrom, pos);
+        return snprintf(buf, cap, "(INS) chr: %d, org pos: %u, ref pos: %u, diff: %d\n", l->chrom, pos, r->start,
+                        (int)(r->start - pos));
+    }
+    if (l->type == SVT_DEL) {
+        if (!((uint32_t)SV_MIN_LENGTH < end - pos)) return 0;
+        int n = snprintf(buf, cap, "(DEL) chr: %d, org pos: %u, org end: %u, ref pos: ", l->chrom, pos, end);
+        auto put = [&](const char *fmt, long v) { n += snprintf(buf + n, cap - (size_t)n, fmt, v); };
+        if (r->start == SVT_NA) n += snprintf(buf + n, cap - (size_t)n, "NA, ref end: ");
+        else put("%ld, ref end: ", (long)(int)r->start);
+        if (r->end == SVT_NA) n += snprintf(buf + n, cap - (size_t)n, "NA, ");
+        else put("%ld, ", (long)(int)r->end);
+        if (r->start == SVT_NA) n += snprintf(buf + n, cap - (size_t)n, "diff pos: NA, ");
+        else put("diff pos: %ld, ", (long)(int)(r->start - pos));
+        if (r->end == SVT_NA) n += snprintf(buf + n, cap - (size_t)n, "diff end: NA\n");
+        else put("diff end: %ld\n", (long)(int)(r->end - end));
+        return n;
+    }
+    if (l->type == SVT_INV) {
+        if (!((uint32_t)SV_MIN_LENGTH < end - pos)) return 0;
+        return snprintf(buf, cap, "(INV) chr: %d, org pos: %u, org end: %u, ref pos: %u, ref end: %u\n", l->chrom,
+                        pos, end, r->start, r->end);
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,98 @@
+"""ctypes bindings of libsvtrek_host.so: BAM ingest, VCF record parsing, result printing."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from ._lib import LOCUS_DTYPE, PKG, SvtPileupView
+from .pileup import Pileup
+
+_host = None
+
+
+def load_host() -> C.CDLL:
+    global _host
+    if _host is None:
+        path = os.path.join(PKG, "libsvtrek_host.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"host library not built: {path}")
+        L = C.CDLL(path)
+        P = C.c_void_p
+        L.svth_bam_read.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_size_t]
+        L.svth_bam_read.restype = P
+        L.svth_bam_free.argtypes = [P]
+        L.svth_bam_free.restype = None
+        L.svth_bam_view.argtypes = [P, C.POINTER(SvtPileupView)]
+        L.svth_bam_view.restype = None
+        L.svth_bam_n_targets.argtypes = [P]
+        L.svth_bam_n_targets.restype = C.c_int32
+        L.svth_bam_target_name.argtypes = [P, C.c_int32]
+        L.svth_bam_target_name.restype = C.c_char_p
+        L.svth_bam_n_records.argtypes = [P]
+        L.svth_bam_n_records.restype = C.c_int64
+        L.svth_bam_n_cg_restored.argtypes = [P]
+        L.svth_bam_n_cg_restored.restype = C.c_int64
+        L.svth_parse_line.argtypes = [C.c_char_p, P, C.c_char_p, C.c_size_t]
+        L.svth_parse_line.restype = C.c_int
+        L.svth_format.argtypes = [P, P, C.c_char_p, C.c_size_t]
+        L.svth_format.restype = C.c_int
+        L.svth_is_unknown_type.argtypes = [P]
+        L.svth_is_unknown_type.restype = C.c_int
+        _host = L
+    return _host
+
+
+def read_bam(path: str, threads: int = 4) -> tuple[Pileup, dict]:
+    L = load_host()
+    err = C.create_string_buffer(512)
+    h = L.svth_bam_read(path.encode(), threads, err, 512)
+    if not h:
+        raise OSError(err.value.decode())
+    try:
+        v = SvtPileupView()
+        L.svth_bam_view(h, C.byref(v))
+        nt = v.n_targets
+
+        def arr(p, dtype, n):
+            if n == 0 or not p:
+                return np.zeros(0, dtype=dtype)
+            return np.frombuffer((C.c_char * (n * np.dtype(dtype).itemsize)).from_address(p), dtype=dtype).copy()
+
+        tid_off = arr(v.tid_off, np.int64, nt + 1)
+        if nt == 0:
+            tid_off = np.zeros(1, dtype=np.int64)
+        nr = int(tid_off[-1])
+        cig_off = arr(v.cig_off, np.uint64, nr + 1)
+        if len(cig_off) == 0:
+            cig_off = np.zeros(1, dtype=np.uint64)
+        pl = Pileup(tid_off=tid_off, pos=arr(v.pos, np.int32, nr), endpos=arr(v.endpos, np.int32, nr),
+                    cig_off=cig_off, cigar=arr(v.cigar, np.uint32, int(cig_off[-1])),
+                    clip=arr(v.clip, np.uint8, nr))
+        info = {"names": [L.svth_bam_target_name(h, t).decode() for t in range(nt)],
+                "records": int(L.svth_bam_n_records(h)), "cg_restored": int(L.svth_bam_n_cg_restored(h))}
+        return pl, info
+    finally:
+        L.svth_bam_free(h)
+
+
+def parse_line(line: str):
+    """-> (action, (type, chrom, pos, end) | None, stderr_text)"""
+    L = load_host()
+    buf = C.create_string_buffer(line.encode("latin-1"))
+    loc = np.zeros(1, dtype=LOCUS_DTYPE)
+    err = C.create_string_buffer(1024)
+    act = L.svth_parse_line(buf, loc.ctypes.data, err, 1024)
+    rec = tuple(int(x) for x in loc[0]) if act == 1 else None
+    return act, rec, err.value.decode("latin-1")
+
+
+def format_result(locus: np.void, result: np.void) -> str:
+    from ._lib import RESULT_DTYPE
+    L = load_host()
+    lo = np.array([locus], dtype=LOCUS_DTYPE)
+    r = np.array([result], dtype=RESULT_DTYPE)
+    buf = C.create_string_buffer(512)
+    n = L.svth_format(lo.ctypes.data, r.ctypes.data, buf, 512)
+    return buf.raw[:n].decode("latin-1")

@@ -1,0 +1,90 @@
+"""End to end: `svtrek audt -b BAM -v VCF` (CLI -> BAM ingest -> C ABI -> HIP) prints
+exactly what the CPU oracle's restatement of the reference audit prints."""
+import os
+import random
+import subprocess
+
+import oracle_ffi as O
+import pytest
+
+from svtrek_amd import sim
+from svtrek_amd.simvcf import resolved_vcf_from_loci, simulate
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "svtrek_amd", "svtrek")
+
+
+def run_cli(*args, check=True):
+    r = subprocess.run([CLI, "audt", *args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=300)
+    if check and r.returncode != 0:
+        raise AssertionError(f"svtrek failed rc={r.returncode}\n{r.stderr}")
+    return r
+
+
+def test_cfg1_simvcf_layout(tmp_path):
+    """BASELINE config 1: 100 DEL via the simvcf transform + 10x long-read BAM, -t 1."""
+    r = sim.generate(sim.WORKLOADS["cfg1_100del_10x"], keep_handle=True)
+    bam = str(tmp_path / "cfg1.bam")
+    sim.write_bam(r, bam, with_seq=True)
+    resolved = resolved_vcf_from_loci(r.loci, r.truth, seed=1)
+    vcf_text = "".join(simulate(resolved, random.Random(101)))
+    vcf = tmp_path / "cfg1.sim.vcf"
+    vcf.write_text(vcf_text)
+    out = run_cli("-b", bam, "-v", str(vcf), "-t", "1").stdout
+    want = O.audit_text(vcf_text, r.pileup)
+    assert out == want
+    dels = [l for l in out.splitlines() if l.startswith("(DEL)")]
+    assert len(dels) == 100
+    # END= matched inside CIEND=: every end window is empty -> "ref end: NA" 
+    assert all("ref end: NA" in l for l in dels)
+    assert sum("ref pos: NA" not in l for l in dels) > 50
+
+
+def test_plain_vcf_mixed_types_and_errors(tmp_path):
+    r = sim.generate(sim.SimConfig(seed=31, n_targets=2, n_loci=300, del_frac=0.5, coverage=20,
+                                   p_clip_ends=0.2), keep_handle=True)
+    bam = str(tmp_path / "x.bam")
+    sim.write_bam(r, bam, with_seq=False)
+    vcf = tmp_path / "x.vcf"
+    sim.write_vcf(r.loci, str(vcf), chrom_prefix="chr")
+    extra = ("chr1\t30000\tinv1\tN\t<INV>\t.\tPASS\tSVTYPE=INV;END=36000\n"
+             "chr1\t40000\tdup1\tN\t<DUP>\t.\tPASS\tSVTYPE=DUP;END=46000\n"
+             "chr1\tabc\tbad\tN\t<DEL>\t.\tPASS\tSVTYPE=DEL;END=46000\n"
+             "chr2\t50000\tdel50\tN\t<DEL>\t.\tPASS\tSVTYPE=DEL;END=50050\n"
+             "chr2\t50000\tdel49\tN\t<DEL>\t.\tPASS\tSVTYPE=DEL;END=50049\n"
+             "chr9\t50000\tnocontig\tN\t<DEL>\t.\tPASS\tSVTYPE=DEL;END=60000\n"
+             "onlyone\n"
+             "x\n")
+    text = vcf.read_text() + extra
+    vcf.write_text(text)
+    res = run_cli("-b", bam, "-v", str(vcf), "-t", "3")
+    assert res.stdout == O.audit_text(text, r.pileup)
+    assert "[ERROR] Unkown type." in res.stderr
+    assert "[ERROR] Conversion error to pos abc" in res.stderr
+    assert "VCF: no index at line: onlyone" in res.stderr
+
+
+def test_nondefault_flags(tmp_path):
+    r = sim.generate(sim.SimConfig(seed=41, n_targets=1, n_loci=120, del_frac=0.5, coverage=25), keep_handle=True)
+    bam = str(tmp_path / "y.bam")
+    sim.write_bam(r, bam)
+    vcf = tmp_path / "y.vcf"
+    sim.write_vcf(r.loci, str(vcf))
+    from svtrek_amd import Params
+    p = Params(wider_interval=5000, median_interval=3000, narrow_interval=800, consensus_interval_range=300,
+               consensus_interval=8, consensus_min_count=4)
+    out = run_cli("-b", bam, "--vcf", str(vcf), "--wider-interval", "5000", "--median-interval", "3000",
+                  "--narrow-interval", "800", "--consensus-interval-range", "300", "--consensus-interval", "8",
+                  "--consensus-min-count", "4", "--batch", "17").stdout
+    assert out == O.audit_text(vcf.read_text(), r.pileup, p)
+
+
+def test_cli_usage_and_missing_files(tmp_path):
+    r = subprocess.run([CLI], stdout=subprocess.PIPE, text=True)
+    assert r.returncode == 1 and r.stdout.startswith("Usage: ./svtrek [MODE] [OPTIONS]")
+    r = subprocess.run([CLI, "audt", "-h"], stdout=subprocess.PIPE, text=True)
+    assert r.returncode == 0 and "--consensus-min-count" in r.stdout
+    r = run_cli("-v", str(tmp_path / "none.vcf"), check=False)
+    assert r.returncode != 0 and "[ERROR] BAM file is not provided." in r.stderr

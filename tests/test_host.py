@@ -1,0 +1,165 @@
+"""CPU tests of the host side: BAM ingest round trip, VCF parsing (A1) and printing (A11)
+against the oracle restatement, the simvcf golden fixtures, and the C-ABI symbol table."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import oracle_ffi as O
+import pytest
+
+from svtrek_amd import host, sim
+from svtrek_amd._lib import ENGINE_SYMBOLS, LOCUS_DTYPE, RESULT_DTYPE, SVT_NA
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def test_engine_library_exports_every_header_symbol():
+    """libsvtrek_hip.so loads (no GPU needed) and exports every svt_* the header declares."""
+    hdr = open(os.path.join(ROOT, "include", "svtrek_gpu.h")).read()
+    declared = set(re.findall(r"\b(svt_[a-z_]+)\s*\(", hdr))
+    assert declared == set(ENGINE_SYMBOLS), declared ^ set(ENGINE_SYMBOLS)
+    lib = C.CDLL(os.path.join(ROOT, "svtrek_amd", "libsvtrek_hip.so"))
+    for s in declared:
+        assert hasattr(lib, s), s
+    lib.svt_version.restype = C.c_char_p
+    assert b"gfx950" in lib.svt_version()
+
+
+def test_host_library_exports():
+    hdr = open(os.path.join(ROOT, "svtrek_amd", "csrc", "svtrek_host.h")).read()
+    L = host.load_host()
+    for s in set(re.findall(r"\b(svth_[a-z_0-9]+)\s*\(", hdr)):
+        assert hasattr(L, s), s
+
+
+@pytest.mark.parametrize("with_seq", [False, True])
+def test_bam_roundtrip(tmp_path, with_seq):
+    cfg = sim.SimConfig(seed=5, n_targets=3, n_loci=30, del_frac=0.5, coverage=8, p_clip_ends=0.3,
+                        p_exotic=0.05)
+    r = sim.generate(cfg, keep_handle=True)
+    path = str(tmp_path / "x.bam")
+    sim.write_bam(r, path, with_seq=with_seq)
+    pl, info = host.read_bam(path, threads=3)
+    assert info["names"] == ["1", "2", "3"]
+    assert info["records"] == r.pileup.n_reads
+    src = r.pileup
+    np.testing.assert_array_equal(pl.tid_off, src.tid_off)
+    np.testing.assert_array_equal(pl.pos, src.pos)
+    np.testing.assert_array_equal(pl.endpos, src.endpos)
+    np.testing.assert_array_equal(pl.cig_off, src.cig_off)
+    np.testing.assert_array_equal(pl.cigar, src.cigar)
+    # clip bits derived from the CIGAR words (n_cigar >= 1 everywhere here)
+    last = (src.cigar[src.cig_off[1:].astype(np.int64) - 1] & 15) == 4
+    first = (src.cigar[src.cig_off[:-1].astype(np.int64)] & 15) == 4
+    np.testing.assert_array_equal(pl.clip, last.astype(np.uint8) | (first.astype(np.uint8) << 1))
+
+
+def test_bam_long_cigar_cg_tag(tmp_path):
+    """> 65535 CIGAR ops are stored as kSmN + CG:B,I; ingest restores them (htslib bam_tag2cigar)."""
+    cfg = sim.SimConfig(seed=8, n_targets=1, n_loci=4, coverage=2.0, read_len_mean=200000, read_len_sd=0,
+                        read_len_min=150000, rho=1.5, spacing=400000)
+    r = sim.generate(cfg, keep_handle=True)
+    nops = np.diff(r.pileup.cig_off.astype(np.int64))
+    assert nops.max() > 65535
+    path = str(tmp_path / "long.bam")
+    sim.write_bam(r, path, with_seq=False)
+    pl, info = host.read_bam(path, threads=2)
+    assert info["cg_restored"] == int((nops > 65535).sum())
+    np.testing.assert_array_equal(pl.cigar, r.pileup.cigar)
+    np.testing.assert_array_equal(pl.endpos, r.pileup.endpos)
+
+
+def _vcf_lines(path):
+    with open(path) as f:
+        for line in f:
+            if len(line) < 2 or line.startswith("#"):
+                continue
+            yield line.rstrip("\n")
+
+
+@pytest.mark.parametrize("seed", [1, 7, 2024])
+def test_parse_simvcf_golden(seed):
+    """Reference simvcf.py output (fixture): product parser == oracle parser; the
+    END= match inside CIEND= gives every DEL a huge uint32 end."""
+    n_del = 0
+    for line in _vcf_lines(os.path.join(GOLD, f"simvcf_seed{seed}.sim.vcf")):
+        a1 = host.parse_line(line)
+        a2 = O.parse_line(line)
+        assert a1[0] == a2[0] and a1[1] == a2[1], (line, a1, a2)
+        if a1[0] == 1 and a1[1][0] == 2:
+            n_del += 1
+            ciend = int(re.search(r"CIEND=(-?\d+)", line).group(1))
+            assert a1[1][3] == ciend & 0xFFFFFFFF
+    assert n_del > 0
+
+
+def _fuzz_line(rng):
+    chrom = rng.choice(["1", "chr2", "chrX", "X", "0", "-1", "22", "chr07", " 3"])
+    pos = rng.choice(["0", "00", "12345", "-5", "abc", " 7", "4294967296", "99999999999", "1e3", "60000"])
+    ref = rng.choice(["N", "A", "ACGT" * 13, "ACGT" * 12 + "AC", "ACGT" * 12 + "ACG"])
+    alt = rng.choice(["<DEL>", "N", "A", "A,C", "A" * 51, "A" * 50, "AC,A" + "G" * 60, ",,A"])
+    keys = []
+    if rng.random() < 0.8:
+        keys.append("SVTYPE=" + rng.choice(["DEL", "INS", "INV", "DUP", "TRA", "BND", "DEL:ME", "INS:ME",
+                                             "del", "CNV", "AVERYLONGTYPENAMEHERE", ""]))
+    if rng.random() < 0.5:
+        keys.append("CIEND=" + rng.choice(["-40,25", "0,0", "x"]))
+    if rng.random() < 0.7:
+        keys.append("END=" + rng.choice(["60100", "60050", "60049", "0", "abc", "-3", "999999999999999999999999999999999999"]))
+    if rng.random() < 0.2:
+        keys.append("SVEND=5")
+    rng.shuffle(keys)
+    info = ";".join(keys) if keys else "."
+    fields = [chrom, pos, "id", ref, alt, "60", "PASS", info]
+    if rng.random() < 0.3:
+        fields += ["GT", "0/1"]
+    sep = "\t\t" if rng.random() < 0.05 else "\t"
+    return sep.join(fields)
+
+
+def test_parse_fuzz_vs_oracle():
+    import random
+    rng = random.Random(42)
+    seen = set()
+    for _ in range(4000):
+        line = _fuzz_line(rng)
+        a1 = host.parse_line(line)
+        a2 = O.parse_line(line)
+        assert a1[0] == a2[0] and a1[1] == a2[1], (line, a1, a2)
+        seen.add(a1[0])
+    assert seen == {0, 1, 2}
+
+
+def test_format_vs_oracle():
+    rng = np.random.default_rng(0)
+    for _ in range(3000):
+        t = int(rng.choice([1, 2, 3, 4, 0]))
+        pos = int(rng.integers(0, 2**32))
+        end = (pos + int(rng.choice([49, 50, 51, 1000, -5]))) & 0xFFFFFFFF
+        loc = np.array([(t, int(rng.integers(-2, 25)), pos, end)], dtype=LOCUS_DTYPE)[0]
+        vals = [SVT_NA, int(rng.integers(0, 2**32)), (pos + int(rng.integers(-600, 600))) & 0xFFFFFFFF]
+        res = np.array([(int(rng.choice(vals)), int(rng.choice(vals)))], dtype=RESULT_DTYPE)[0]
+        a = host.format_result(loc, res)
+        lo = np.array([loc], dtype=LOCUS_DTYPE)
+        rr = np.array([res], dtype=RESULT_DTYPE)
+        buf = C.create_string_buffer(512)
+        n = O.lib().orc_format_result(lo.ctypes.data, rr.ctypes.data, buf, 512)
+        assert a == buf.raw[:n].decode(), (loc, res)
+
+
+def test_format_examples():
+    loc = np.array([(2, 1, 1000, 5000)], dtype=LOCUS_DTYPE)[0]
+    res = np.array([(1003, SVT_NA)], dtype=RESULT_DTYPE)[0]
+    assert host.format_result(loc, res) == ("(DEL) chr: 1, org pos: 1000, org end: 5000, ref pos: 1003, "
+                                            "ref end: NA, diff pos: 3, diff end: NA\n")
+    loc = np.array([(1, 3, 2000, 2001)], dtype=LOCUS_DTYPE)[0]
+    assert host.format_result(loc, np.array([(1990, SVT_NA)], dtype=RESULT_DTYPE)[0]) == \
+        "(INS) chr: 3, org pos: 2000, ref pos: 1990, diff: -10\n"
+    loc = np.array([(3, 1, 100, 900)], dtype=LOCUS_DTYPE)[0]
+    assert host.format_result(loc, np.array([(SVT_NA, SVT_NA)], dtype=RESULT_DTYPE)[0]) == \
+        "(INV) chr: 1, org pos: 100, org end: 900, ref pos: 4294967295, ref end: 4294967295\n"
+    # a DEL of exactly 50 bp reaches the switch but prints nothing (audit.c:190)
+    loc = np.array([(2, 1, 100, 150)], dtype=LOCUS_DTYPE)[0]
+    assert host.format_result(loc, np.array([(SVT_NA, SVT_NA)], dtype=RESULT_DTYPE)[0]) == ""

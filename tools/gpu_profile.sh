@@ -1,0 +1,27 @@
+#!/bin/bash
+# Run ON THE GPU BOX (via gpurun): kernel trace + stats and HBM PMC passes of bench.py.
+#   tools/gpu_profile.sh TAG [bench args...]
+# Writes gpurun_out/prof_TAG/{trace,pmc_fetch,pmc_write}/ and bench logs.  Every GPU step
+# has its own time limit and the script stops at the first failing step.
+set -u
+TAG=${1:?tag}; shift
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+ARGS=("$@")
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] $name" >> "$OUT/steps.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >> "$OUT/steps.log"
+  if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc"; tail -20 "$OUT/$name.log"; exit $rc; fi
+}
+step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+  python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline "${ARGS[@]}"
+step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+  python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "${ARGS[@]}"
+step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+  python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "${ARGS[@]}"
+echo "profile $TAG done"
