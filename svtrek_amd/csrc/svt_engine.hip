@@ -1,20 +1,28 @@
 // svt_engine.hip -- MI355X (gfx950) SV-refinement engine: HIP kernels + the C ABI of
 // include/svtrek_gpu.h.
 //
-// One wavefront (one 64-lane workgroup) per SV locus.  Per query window the wave
-//   1. finds the candidate read range with two 64-ary searches over HBM-resident,
-//      per-contig pos[] (sorted) and emax[] (prefix max of endpos) arrays   -- A3
-//   2. tests 64 reads per step against htslib's overlap rule (16-B records, coalesced)
-//   3. walks each yielded read's CIGAR 64 ops per step: one coalesced 256-B load, a DPP
-//      inclusive prefix scan of the reference advance gives every op's reference
-//      position at once, a ballot finds the first op past the window end (the break of
-//      refinement.c:145-148), and ballots compact the breakpoint candidates into LDS -- A4..A6
-//   4. bitonic-sorts the candidates in LDS and runs consensus_pos's asymmetric vote with
-//      per-element cluster counts computed in parallel (binary search + int64 prefix
-//      sums) and the greedy accept done with scalar readlanes                      -- A8..A10
-// Windows with more than SVT_LDS_CANDS candidates re-run the same code on a slab taken
-// from a device spill pool, so results stay exact.  No floating point anywhere; no MFMA
-// (integer scan + vote, HBM/latency bound).
+// One wavefront (one 64-lane workgroup) per query WINDOW (a DEL locus has two: the
+// refine_start and refine_end windows; an INS locus one).  Per window the wave
+//   1. finds the yielded read range [lo, hi) of htslib's region query (A3) with a
+//      bucket index (first read per 4 kb of contig) + one 64-lane probe each for the
+//      sorted pos[] and the prefix-max-of-endpos emax[] arrays;
+//   2. streams the window's CIGAR words -- the reads [lo, hi) own ONE contiguous span
+//      of the CIGAR arena -- in 256-op tiles, one 16-B load per lane (1 KiB per wave
+//      instruction, fully coalesced, next tile prefetched while the current one is
+//      voted on).  A segmented wave prefix scan (DPP) of the reference advance, reset at
+//      each read's first op to its pos, gives every op's walk position at once; because
+//      the walk position only grows inside a read, "this op comes after the break of
+//      refinement.c:145-148" is just `position before the op > inter.end`, so no second
+//      scan is needed.  Breakpoint candidates (A4-A6) and the soft-clip candidates of
+//      each read's stop op are compacted into LDS with ballots; tails of reads that
+//      already broke (and reads that do not overlap the window) are skipped;
+//   3. bitonic-sorts the candidates in LDS and runs consensus_pos's asymmetric vote
+//      (A8-A10): per-element cluster counts in parallel (binary search + int64 prefix
+//      sums), the greedy accept with scalar readlanes.
+// Windows with more than SVT_LDS_CANDS candidates re-run on a slab of a device spill
+// pool (exact).  Reads whose walk could wrap uint32 go through a per-read wave walk
+// (walk_read) that replays the reference's uint32 arithmetic op by op.  No floating
+// point, no MFMA: integer scan + vote, HBM-streaming bound.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -22,28 +30,38 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.1.0 (gfx950)"
+#define SVT_VERSION "svtrek_amd 0.2.0 (gfx950, window-stream kernel)"
 
 namespace {
 
 constexpr int WAVE = 64;
+constexpr int TILE = 256;                   // CIGAR ops per stream step (4 per lane)
 constexpr int CAP = SVT_LDS_CANDS;          // LDS candidates per window
 constexpr int SV_MIN_LENGTH = 50;           // params.h:33
 constexpr uint32_t OP_INS = 1, OP_DEL = 2, OP_SOFT = 4;   // params.h:11-14
 constexpr int K_START = 0, K_END = 1, K_INS = 2;          // refine_start / refine_end / refine_ins
 constexpr int32_t T_INS = 1, T_DEL = 2;
+constexpr int BKT_SHIFT = 12;               // read-start bucket = 4096 bp
+constexpr uint32_t NCIG_MASK = 0x1fffffffu; // rec.z: n_cigar | slow << 29 | clip << 30
+constexpr uint32_t SLOW_BIT = 1u << 29;
+constexpr uint32_t CIGAR_PAD = 260;         // zero words after the arena (tile over-read)
 
 struct DevPileup {
-    const int32_t *pos;      // [n_reads]
-    const int32_t *emax;     // [n_reads] prefix max of endpos within the contig
-    const uint4 *rec;        // [n_reads] {endpos, n_cig | clip<<30, cig_off lo, cig_off hi}
-    const int64_t *tid_off;  // [n_targets+1]
-    const uint32_t *cigar;
+    const int32_t *pos;       // [n_reads]
+    const int32_t *emax;      // [n_reads] prefix max of endpos within the contig
+    const uint4 *rec;         // [n_reads] {pos, endpos, n_cig | slow<<29 | clip<<30, cig_off low 32}
+    const uint64_t *off64;    // [n_reads+1] cig_off
+    const int64_t *tid_off;   // [n_targets+1]
+    const int64_t *bkt_off;   // [n_targets+1] start of each contig's bucket table
+    const uint32_t *bkt;      // first contig-relative read index with pos >= b << BKT_SHIFT
+    const int32_t *maxspan;   // [n_targets] max(endpos - pos)
+    const uint32_t *cigar;    // padded by CIGAR_PAD zero words
     int32_t n_targets;
 };
 
@@ -56,7 +74,7 @@ struct KArgs {
     KParams prm;
     const svt_locus *loci;
     svt_result *out;
-    uint32_t n;
+    uint32_t n;                 // loci
     int32_t *pool;              // spill slabs (int32 words)
     unsigned long long *pool_head;
     unsigned long long pool_words;
@@ -66,12 +84,8 @@ struct KArgs {
 
 // ------------------------------------------------------------------ wave primitives
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
-
 __device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
-
-__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ __forceinline__ int32_t rdlane_i(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     uint32_t lo = rdlane((uint32_t)v, l), hi = rdlane((uint32_t)(v >> 32), l);
@@ -79,17 +93,52 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
 }
 __device__ __forceinline__ int32_t uniform_i(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Inclusive wave64 prefix sum (mod 2^32) with DPP: row_shr 1/2/4/8 inside each 16-lane
-// row, then row_bcast:15 (rows 1,3) and row_bcast:31 (rows 2,3).
-__device__ __forceinline__ uint32_t wave_scan_add(uint32_t x) {
-    uint32_t v = x;
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xf, false);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int32_t dpp_i(int32_t v, int32_t identity) {
+    return __builtin_amdgcn_update_dpp(identity, v, CTRL, ROWMASK, 0xf, false);
+}
+// DPP controls (GFX9): row_shr:n = 0x110+n, wave_shr:1 = 0x138, row_bcast:15 = 0x142, row_bcast:31 = 0x143
+
+// Inclusive wave64 prefix sum (mod 2^32).
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += dpp<0x111, 0xf>(v);
+    v += dpp<0x112, 0xf>(v);
+    v += dpp<0x114, 0xf>(v);
+    v += dpp<0x118, 0xf>(v);
+    v += dpp<0x142, 0xa>(v);
+    v += dpp<0x143, 0xc>(v);
     return v;
+}
+
+// Inclusive wave64 max scan (identity -1).
+__device__ __forceinline__ int32_t wave_scan_max(int32_t v) {
+    v = max(v, dpp_i<0x111, 0xf>(v, -1));
+    v = max(v, dpp_i<0x112, 0xf>(v, -1));
+    v = max(v, dpp_i<0x114, 0xf>(v, -1));
+    v = max(v, dpp_i<0x118, 0xf>(v, -1));
+    v = max(v, dpp_i<0x142, 0xa>(v, -1));
+    v = max(v, dpp_i<0x143, 0xc>(v, -1));
+    return v;
+}
+
+// Inclusive segmented wave64 scan of (head, value): a head restarts the running sum.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void seg_step(uint32_t &h, uint32_t &v) {
+    uint32_t hs = dpp<CTRL, ROWMASK>(h), vs = dpp<CTRL, ROWMASK>(v);
+    v = h ? v : v + vs;
+    h |= hs;
+}
+__device__ __forceinline__ void wave_seg_scan(uint32_t &h, uint32_t &v) {
+    seg_step<0x111, 0xf>(h, v);
+    seg_step<0x112, 0xf>(h, v);
+    seg_step<0x114, 0xf>(h, v);
+    seg_step<0x118, 0xf>(h, v);
+    seg_step<0x142, 0xa>(h, v);
+    seg_step<0x143, 0xc>(h, v);
 }
 
 __device__ __forceinline__ int64_t wave_scan_add64(int64_t x) {
@@ -107,23 +156,17 @@ template <typename Pred>
 __device__ __forceinline__ int64_t wave_partition_point(int64_t l, int64_t h, Pred pred) {
     const int ln = lane_id();
     while (h - l > WAVE) {
-        // probe 64 evenly spaced points p_k = l + (k+1)*(h-l)/65, k = 0..63
         int64_t span = h - l;
         int64_t p = l + ((int64_t)(ln + 1) * span) / (WAVE + 1);
-        bool t = pred(p);
-        uint64_t m = ballot(t);
-        // all probes before the first true probe are false
+        uint64_t m = ballot(pred(p));
         int k = m ? __builtin_ctzll(m) : WAVE;
         int64_t nl = k == 0 ? l : l + ((int64_t)k * span) / (WAVE + 1) + 1;
         int64_t nh = k == WAVE ? h : l + ((int64_t)(k + 1) * span) / (WAVE + 1) + 1;
-        if (nh > h) nh = h;
         l = nl;
-        h = nh;
+        h = nh < h ? nh : h;
     }
-    // final: at most 64 elements
     int64_t p = l + ln;
-    bool t = p < h && pred(p);
-    uint64_t m = ballot(t);
+    uint64_t m = ballot(p < h && pred(p));
     return m ? l + __builtin_ctzll(m) : h;
 }
 
@@ -135,23 +178,28 @@ struct Sink {
     __device__ __forceinline__ void push(bool pred, int32_t val) {
         uint64_t m = ballot(pred);
         if (!m) return;
-        int ln = lane_id();
-        int idx = n + __popcll(m & ((1ull << ln) - 1ull));
+        int idx = n + __popcll(m & ((1ull << lane_id()) - 1ull));
         if (pred && idx < cap) buf[idx] = val;
         n += __popcll(m);
     }
 };
 
-template <bool COUNT>
 struct WinStats {
     unsigned long long reads = 0, ops = 0;
 };
 
-// Walk one yielded read's CIGAR (refinement.c:118-159 / :184-221 / :295-318).
+template <int KIND>
+__device__ __forceinline__ bool is_candidate_op(uint32_t op, uint32_t len) {
+    if (KIND == K_INS) return op == OP_INS && (uint32_t)SV_MIN_LENGTH <= len;   // refinement.c:299
+    return op == OP_DEL && (uint32_t)SV_MIN_LENGTH < len;                       // refinement.c:124,:190
+}
+
+// Per-read walk, 64 ops per step, replaying the reference's uint32 position arithmetic
+// exactly (refinement.c:118-159 / :184-221 / :295-318).  Used for reads whose walk could
+// wrap 2^32 (never in practice) and by the per-read gather variant.
 template <int KIND, bool COUNT>
-__device__ __forceinline__ void walk_read(const uint32_t *__restrict__ cigar, uint64_t off, uint32_t n,
-                                          uint32_t rpos, uint32_t clip, uint32_t s, uint32_t e,
-                                          Sink &sink, WinStats<COUNT> &st) {
+__device__ __forceinline__ void walk_read(const uint32_t *__restrict__ cigar, uint64_t off, uint32_t n, uint32_t rpos,
+                          uint32_t clip, uint32_t s, uint32_t e, Sink &sink, WinStats &st) {
     const int ln = lane_id();
     uint32_t carry = rpos;
     bool broke = false;
@@ -160,19 +208,15 @@ __device__ __forceinline__ void walk_read(const uint32_t *__restrict__ cigar, ui
     for (uint32_t cb = 0; cb < n; cb += WAVE) {
         uint32_t i = cb + (uint32_t)ln;
         bool v = i < n;
-        uint32_t w = v ? __builtin_nontemporal_load(cigar + off + i) : 0u;
+        uint32_t w = v ? cigar[off + i] : 0u;
         uint32_t op = w & 0xfu, len = w >> 4;
         uint32_t adv = (op != OP_INS && op != OP_SOFT) ? len : 0u;   // refinement.c:141
         uint32_t after = carry + wave_scan_add(adv);
         uint32_t before = after - adv;
         uint64_t bm = ballot(v && after > e);                         // refinement.c:145
         int fb = bm ? __builtin_ctzll(bm) : WAVE;
-        bool in = v && ln <= fb;
-        bool hit;
-        if (KIND == K_INS) hit = in && op == OP_INS && (uint32_t)SV_MIN_LENGTH <= len;   // :299
-        else hit = in && op == OP_DEL && (uint32_t)SV_MIN_LENGTH < len;                 // :124,:190
-        int32_t val = KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before;   // :198/:136
-        sink.push(hit, val);
+        bool hit = v && ln <= fb && is_candidate_op<KIND>(op, len);
+        sink.push(hit, KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before);   // :198 / :136
         if (bm) {
             broke = true;
             stop_rp = rdlane(after, fb);
@@ -198,40 +242,236 @@ __device__ __forceinline__ void walk_read(const uint32_t *__restrict__ cigar, ui
     }
 }
 
-// Region query + walks of one window; returns candidates seen (sink.n).
+// ------------------------------------------------------------------ read range (A3)
+// First contig-relative read index with pos >= X (X >= 0), via the bucket table.
+__device__ __forceinline__ int64_t first_pos_ge(const DevPileup &P, int tid, int64_t ra, int64_t nr, int64_t X) {
+    const int64_t b0 = P.bkt_off[tid], nb = P.bkt_off[tid + 1] - b0;
+    int64_t b = X >> BKT_SHIFT;
+    if (b >= nb - 1) return nr;                 // past the last read start
+    int64_t l = P.bkt[b0 + b], h = P.bkt[b0 + b + 1];
+    const int32_t *pos = P.pos + ra;
+    return wave_partition_point(l, h, [&](int64_t r) { return (int64_t)pos[r] >= X; });
+}
+
+// sam_itr_queryi(idx, chrom-1, inter.start-1, inter.end-1) (refinement.c:114): the
+// reads [lo, hi) of contig tid may overlap [beg, end); each still needs endpos > beg.
+__device__ __forceinline__ bool read_range(const DevPileup &P, int tid, int64_t beg, int64_t end, int64_t &lo,
+                                           int64_t &hi) {
+    if (tid < 0 || tid >= P.n_targets || end <= beg) return false;   // no reads (A3)
+    const int64_t ra = P.tid_off[tid], nr = P.tid_off[tid + 1] - ra;
+    if (nr == 0) return false;
+    int64_t h = first_pos_ge(P, tid, ra, nr, end);
+    int64_t lb = beg - (int64_t)P.maxspan[tid];
+    int64_t l0 = lb > 0 ? first_pos_ge(P, tid, ra, nr, lb) : 0;
+    const int32_t *emax = P.emax + ra;
+    int64_t l = wave_partition_point(l0, h, [&](int64_t r) { return (int64_t)emax[r] > beg; });
+    lo = ra + l;
+    hi = ra + h;
+    return lo < hi;
+}
+
+// ------------------------------------------------------------------ per-read gather (v1)
 template <int KIND, bool COUNT>
-__device__ int32_t gather_window(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
-                                 WinStats<COUNT> &st) {
-    // sam_itr_queryi(idx, chrom-1, inter.start-1, inter.end-1), refinement.c:114
+__device__ __forceinline__ int32_t gather_perread(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
-    if (tid < 0 || tid >= P.n_targets || end <= beg) return sink.n;   // no reads (A3)
-    const int64_t ra = P.tid_off[tid], rb = P.tid_off[tid + 1];
-    const int32_t *pos = P.pos;
-    const int32_t *emax = P.emax;
-    int64_t hi = wave_partition_point(ra, rb, [&](int64_t r) { return (int64_t)pos[r] >= end; });
-    int64_t lo = wave_partition_point(ra, hi, [&](int64_t r) { return (int64_t)emax[r] > beg; });
+    int64_t lo, hi;
+    if (!read_range(P, tid, beg, end, lo, hi)) return sink.n;
     const int ln = lane_id();
     for (int64_t base = lo; base < hi; base += WAVE) {
         int64_t r = base + ln;
         bool valid = r < hi;
         uint4 rc = valid ? P.rec[r] : make_uint4(0, 0, 0, 0);
-        int32_t rp = valid ? pos[r] : 0;
-        bool ov = valid && (int64_t)(int32_t)rc.x > beg;   // pos < end holds below hi (hts_itr_next)
+        bool ov = valid && (int64_t)(int32_t)rc.y > beg;   // pos < end holds below hi (hts_itr_next)
         uint64_t m = ballot(ov);
         while (m) {
             int l = __builtin_ctzll(m);
             m &= m - 1;
-            uint32_t rpos = rdlane((uint32_t)rp, l);
-            uint32_t nc = rdlane(rc.y, l);
-            uint64_t off = ((uint64_t)rdlane(rc.w, l) << 32) | rdlane(rc.z, l);
-            walk_read<KIND, COUNT>(P.cigar, off, nc & 0x3fffffffu, rpos, nc >> 30, s, e, sink, st);
+            uint32_t z = rdlane(rc.z, l);
+            walk_read<KIND, COUNT>(P.cigar, P.off64[base + l], z & NCIG_MASK, rdlane(rc.x, l), z >> 30, s, e, sink,
+                                   st);
         }
     }
     return sink.n;
 }
 
+// ------------------------------------------------------------------ window stream (v2)
+struct StreamLds {
+    int8_t head[TILE + 8];   // per tile op: block-relative read index of a read's first op, else -1
+};
+
+template <int KIND, bool COUNT>
+__device__ __forceinline__ int32_t gather_stream(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
+                                 StreamLds &L) {
+    // Positions in the stream stay below 2^32 (no wrap) when inter.end < 2^31 and every
+    // streamed read walks less than 2^31 (the others are flagged slow at load time).
+    if (e >= 0x80000000u) return gather_perread<KIND, COUNT>(P, tid, s, e, sink, st);
+    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
+    int64_t lo, hi;
+    if (!read_range(P, tid, beg, end, lo, hi)) return sink.n;
+    const int ln = lane_id();
+    const uint64_t S0 = P.off64[lo];
+    const uint32_t base32 = (uint32_t)S0;
+    const uint32_t *cg = P.cigar;
+    const uint32_t dead_rp = e + 1u;   // stream start position of reads that yield nothing
+    int32_t *hw = reinterpret_cast<int32_t *>(L.head);
+
+    for (int64_t rb = lo; rb < hi; rb += WAVE) {
+        // ---- one block of up to 64 reads, lane k <-> read rb + k
+        const int64_t r = rb + ln;
+        const bool inb = r < hi;
+        const uint4 rc = inb ? P.rec[r] : make_uint4(0, 0, 0, 0);
+        const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
+        const bool slow = (rc.z & SLOW_BIT) != 0;
+        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
+        const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op
+        const int32_t en0 = st0 + (int32_t)ncig;
+        const bool live = ovl && !slow && ncig > 0;
+        const uint32_t hrp = live ? rpos : dead_rp;                 // segment start of this read's walk
+        const int nblk = (int)min<int64_t>(WAVE, hi - rb);
+        const int32_t blk_end = rdlane_i(en0, nblk - 1);
+        const bool has_ops = inb && ncig > 0;
+
+        // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
+        if (KIND != K_INS) {
+            const bool z = ovl && ncig == 0 && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
+            if (KIND == K_START) sink.push(z && (clip & SVT_CLIP_LAST_S), (int32_t)rpos);       // :152
+            else sink.push(z && (clip & SVT_CLIP_FIRST_S), (int32_t)(rpos + 1u));                // :210-220
+        }
+        if (COUNT) {
+            st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
+            if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
+        }
+
+        const uint64_t live_m = ballot(live);
+        int32_t J = live_m ? rdlane_i(st0, __builtin_ctzll(live_m)) : blk_end;
+        uint32_t carry_rp = 0;
+        int32_t carry_k = -1;
+        uint4 wcur = make_uint4(0, 0, 0, 0);
+        int32_t A = 0;
+        if (J < blk_end) {
+            A = (int32_t)(((S0 + (uint64_t)(int64_t)J) & ~3ull) - S0);
+            wcur = *reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)A + 4 * ln);
+        }
+        while (J < blk_end) {
+            const int32_t U = min(A + TILE, blk_end);
+            // ---- head table: which ops start a read
+            hw[ln] = -1;
+            if (ln == 0) hw[WAVE] = -1;
+            __syncthreads();
+            if (has_ops && st0 >= A && st0 <= A + TILE) L.head[st0 - A] = (int8_t)ln;
+            __syncthreads();
+            const int32_t hword = hw[ln];
+            const int32_t hnext = ln == WAVE - 1 ? (int32_t)L.head[TILE] : 0;
+            int32_t hk[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) hk[i] = (int32_t)(int8_t)(hword >> (8 * i));
+            const int32_t nexth0 = __shfl_down(hk[0], 1, WAVE);
+            const uint32_t wv[4] = {wcur.x, wcur.y, wcur.z, wcur.w};
+
+            // ---- local (4 ops) segmented inclusive scan of the reference advance
+            uint32_t op[4], len[4], adv[4], lv[4], lh[4];
+            bool valid[4];
+            uint32_t H = 0, V = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int32_t j = A + 4 * ln + i;
+                valid[i] = j >= J && j < U;
+                op[i] = wv[i] & 0xfu;
+                len[i] = wv[i] >> 4;
+                adv[i] = (valid[i] && op[i] != OP_INS && op[i] != OP_SOFT) ? len[i] : 0u;   // refinement.c:141
+                const bool ishead = valid[i] && hk[i] >= 0;
+                const uint32_t h0 = __shfl(hrp, hk[i] < 0 ? 0 : hk[i], WAVE);
+                if (ishead) { H = 1; V = h0 + adv[i]; }
+                else V += adv[i];
+                lv[i] = V;
+                lh[i] = H;
+            }
+            // ---- wave segmented scan over the lane aggregates, then exclusive per lane
+            uint32_t Hi = H, Vi = V;
+            wave_seg_scan(Hi, Vi);
+            const uint32_t Hx = dpp<0x138, 0xf>(Hi), Vx = dpp<0x138, 0xf>(Vi);
+            const uint32_t pre = Hx ? Vx : carry_rp + Vx;
+            const uint32_t H63 = rdlane(Hi, WAVE - 1), V63 = rdlane(Vi, WAVE - 1);
+            const uint32_t next_carry_rp = H63 ? V63 : carry_rp + V63;
+            // read index of every op (max scan of the head table)
+            int32_t km = -1, kl[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) { km = max(km, valid[i] ? hk[i] : -1); kl[i] = km; }
+            const int32_t kinc = wave_scan_max(km);
+            const int32_t kex = dpp_i<0x138, 0xf>(kinc, -1);
+            const int32_t next_carry_k = max(carry_k, rdlane_i(kinc, WAVE - 1));
+
+            // ---- next tile: continue the read at U unless it already broke / yields nothing
+            int32_t Jn = U;
+            {
+                const int32_t kc = next_carry_k;
+                const bool cont = kc >= 0 && U < rdlane_i(en0, kc);
+                if (!(cont && next_carry_rp <= e)) {
+                    const uint64_t later = kc >= 0 ? (live_m & ~((2ull << kc) - 1ull)) : live_m;
+                    Jn = later ? max(U, rdlane_i(st0, __builtin_ctzll(later))) : blk_end;
+                }
+            }
+            int32_t An = A;
+            uint4 wnext = wcur;
+            if (Jn < blk_end) {   // prefetch while this tile is voted on
+                An = (int32_t)(((S0 + (uint64_t)(int64_t)Jn) & ~3ull) - S0);
+                wnext = *reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)An + 4 * ln);
+            }
+
+            // ---- per op: walk position after / before, break, candidates, stop ops
+            unsigned long long live_ops = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t after = lh[i] ? lv[i] : pre + lv[i];
+                const uint32_t before = after - adv[i];
+                const bool lv_op = valid[i] && before <= e;    // not past this read's break
+                const bool brk = lv_op && after > e;           // the break op itself (refinement.c:145)
+                sink.push(lv_op && is_candidate_op<KIND>(op[i], len[i]),
+                          KIND == K_END ? (int32_t)(before + len[i] + 1u) : (int32_t)before);   // :198 / :136
+                if (COUNT) live_ops += (unsigned long long)__popcll(ballot(lv_op));
+                if (KIND != K_INS) {
+                    const int32_t j = A + 4 * ln + i;
+                    const int32_t hn = i < 3 ? hk[i + 1] : (ln == WAVE - 1 ? hnext : nexth0);
+                    const bool is_last = valid[i] && (j + 1 == blk_end || (j + 1 < A + TILE + 1 && hn >= 0));
+                    const bool stop = brk || (lv_op && is_last);
+                    if (ballot(stop)) {
+                        const int32_t k = max(max(carry_k, kex), kl[i]);
+                        const int32_t kk = k < 0 ? 0 : k;
+                        const uint32_t kclip = (uint32_t)__shfl((int)clip, kk, WAVE);
+                        const uint32_t kpos = (uint32_t)__shfl((int)rpos, kk, WAVE);
+                        if (KIND == K_START)   // trailing S, no break, s <= rp <= e  (refinement.c:152)
+                            sink.push(stop && !brk && (kclip & SVT_CLIP_LAST_S) && s <= after && after <= e,
+                                      (int32_t)after);
+                        else                   // leading S and s <= pos <= e: push rp + 1  (:210-220)
+                            sink.push(stop && (kclip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)kpos &&
+                                          (int64_t)kpos <= (int64_t)e,
+                                      (int32_t)(after + 1u));
+                        if (COUNT && KIND == K_START) live_ops += (unsigned long long)__popcll(ballot(brk && !is_last));
+                    }
+                }
+            }
+            if (COUNT) st.ops += live_ops;
+            carry_rp = next_carry_rp;
+            carry_k = next_carry_k;
+            J = Jn;
+            A = An;
+            wcur = wnext;
+        }
+        // reads whose walk could wrap uint32: exact per-read replay
+        uint64_t sm = ballot(ovl && slow);
+        while (sm) {
+            const int l = __builtin_ctzll(sm);
+            sm &= sm - 1;
+            walk_read<KIND, COUNT>(cg, S0 + (uint64_t)(int64_t)rdlane_i(st0, l), rdlane(ncig, l), rdlane(rpos, l),
+                                   rdlane(clip, l), s, e, sink, st);
+        }
+    }
+    return sink.n;
+}
+
+// ------------------------------------------------------------------ sort + vote (A8-A10)
 // Bitonic sort of buf[0..N) (N power of two, padded with INT32_MAX) by one wave.
-__device__ void wave_bitonic_sort(int32_t *buf, int N) {
+__device__ __forceinline__ void wave_bitonic_sort(int32_t *buf, int N) {
     const int ln = lane_id();
     for (int k = 2; k <= N; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
@@ -250,7 +490,6 @@ __device__ void wave_bitonic_sort(int32_t *buf, int N) {
 
 __device__ __forceinline__ int32_t ref_abs(int32_t a) { return a < 0 ? -a : a; }   // refinement.h:41
 
-// First index in [l, h) of sorted buf with buf[idx] > key  (per-lane binary search)
 __device__ __forceinline__ int32_t first_greater(const int32_t *buf, int32_t l, int32_t h, int64_t key) {
     while (l < h) {
         int32_t m = (l + h) >> 1;
@@ -258,7 +497,6 @@ __device__ __forceinline__ int32_t first_greater(const int32_t *buf, int32_t l, 
     }
     return l;
 }
-// First index in [l, h) with buf[idx] >= key
 __device__ __forceinline__ int32_t first_geq(const int32_t *buf, int32_t l, int32_t h, int64_t key) {
     while (l < h) {
         int32_t m = (l + h) >> 1;
@@ -274,7 +512,7 @@ __device__ __forceinline__ int32_t mean_round(int64_t tot, int32_t cnt) {
 }
 
 // consensus_pos (refinement.c:41-101) on sorted A[0..n) with prefix sums P[0..n].
-__device__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t pos, const KParams &k) {
+__device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t pos, const KParams &k) {
     const int ln = lane_id();
     const int32_t ci = k.ci, range = k.range;
     int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
@@ -340,7 +578,7 @@ __device__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t p
 }
 
 // Sort + prefix sums + vote over buf[0..n) with scratch for P (n+1 int64).
-__device__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k) {
+__device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k) {
     const int ln = lane_id();
     int N = 1;
     while (N < n) N <<= 1;
@@ -360,21 +598,34 @@ __device__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t po
     return vote(buf, P, n, pos, k);
 }
 
-template <int KIND, bool COUNT>
-__device__ int32_t refine_window(const KArgs &a, int32_t *lds_c, int64_t *lds_p, int chrom, uint32_t s,
-                                 uint32_t e, uint32_t imprecise, unsigned long long *wk) {
-    WinStats<COUNT> st;
-    Sink sink{lds_c, CAP, 0};
-    int32_t n = gather_window<KIND, COUNT>(a.pile, chrom - 1, s, e, sink, st);
+struct WinLds {
+    int32_t cand[CAP];
+    int64_t pre[CAP + 1];
+    StreamLds sl;
+};
+
+template <int KIND, bool COUNT, bool STREAM>
+__device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
+                                          StreamLds &L) {
+    if (STREAM) return gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L);
+    return gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+}
+
+template <int KIND, bool COUNT, bool STREAM>
+__device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e, uint32_t imprecise,
+                                 unsigned long long *wk) {
+    WinStats st;
+    Sink sink{lds.cand, CAP, 0};
+    int32_t n = gather<KIND, COUNT, STREAM>(a, chrom - 1, s, e, sink, st, lds.sl);
     if (COUNT && lane_id() == 0) {
         wk[0] += 1; wk[1] += st.reads; wk[2] += st.ops; wk[3] += (unsigned long long)n;
     }
     if (n < a.prm.min_count) return -1;                    // refinement.c:43-45
     if (n <= CAP) {
         __syncthreads();
-        return sort_and_vote(lds_c, lds_p, n, (int32_t)imprecise, a.prm);
+        return sort_and_vote(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm);
     }
-    // spill: take a slab for N ints + (n+1) int64 from the device pool and re-gather
+    // spill: a slab for N ints + (n+1) int64 from the device pool, then re-gather into it
     if (COUNT && lane_id() == 0) wk[4] += 1;
     int N = 1;
     while (N < n) N <<= 1;
@@ -388,43 +639,48 @@ __device__ int32_t refine_window(const KArgs &a, int32_t *lds_c, int64_t *lds_p,
     }
     int32_t *g = a.pool + base;
     int64_t *gp = (int64_t *)(a.pool + ((base + (unsigned long long)N + 1ull) & ~1ull));
-    WinStats<COUNT> st2;
+    WinStats st2;
     Sink s2{g, N, 0};
-    gather_window<KIND, COUNT>(a.pile, chrom - 1, s, e, s2, st2);
+    gather<KIND, false, STREAM>(a, chrom - 1, s, e, s2, st2, lds.sl);
     __syncthreads();
     return sort_and_vote(g, gp, n, (int32_t)imprecise, a.prm);
 }
 
-template <bool COUNT>
+// grid = 2 * n_loci workgroups of one wave: workgroup 2i refines locus i's first window
+// (DEL: refine_start, INS: refine_ins), 2i+1 its second (DEL: refine_end).
+template <bool COUNT, bool STREAM>
 __global__ __launch_bounds__(64) void refine_kernel(KArgs a) {
-    __shared__ int32_t lds_c[CAP];
-    __shared__ int64_t lds_p[CAP + 1];
-    const uint32_t li = blockIdx.x;
+    __shared__ WinLds lds;
+    const uint32_t li = blockIdx.x >> 1, w = blockIdx.x & 1;
     if (li >= a.n) return;
     const svt_locus L = a.loci[li];
     const int32_t type = uniform_i(L.type), chrom = uniform_i(L.chrom);
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
     unsigned long long wk[5] = {0, 0, 0, 0, 0};
-    uint32_t r0 = SVT_NA, r1 = SVT_NA;
+    uint32_t r = SVT_NA;
     const KParams &k = a.prm;
     if (type == T_INS) {                                   // audit.c:176-187
-        uint32_t s = pos - (uint32_t)k.median, e = pos + (uint32_t)k.median;
-        r0 = (uint32_t)refine_window<K_INS, COUNT>(a, lds_c, lds_p, chrom, s, e, pos, wk);
+        if (w == 0) {
+            uint32_t s = pos - (uint32_t)k.median, e = pos + (uint32_t)k.median;
+            r = (uint32_t)refine_window<K_INS, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk);
+        }
     } else if (type == T_DEL) {                            // audit.c:188-220
-        uint32_t bs = pos - (uint32_t)k.wider, be = pos + (uint32_t)k.narrow;
-        uint32_t es = end - (uint32_t)k.narrow, ee = end + (uint32_t)k.narrow;
-        r0 = (uint32_t)refine_window<K_START, COUNT>(a, lds_c, lds_p, chrom, bs, be, pos, wk);
-        __syncthreads();
-        r1 = (uint32_t)refine_window<K_END, COUNT>(a, lds_c, lds_p, chrom, es, ee, end, wk);
+        if (w == 0) {
+            uint32_t s = pos - (uint32_t)k.wider, e = pos + (uint32_t)k.narrow;
+            r = (uint32_t)refine_window<K_START, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk);
+        } else {
+            uint32_t s = end - (uint32_t)k.narrow, e = end + (uint32_t)k.narrow;
+            r = (uint32_t)refine_window<K_END, COUNT, STREAM>(a, lds, chrom, s, e, end, wk);
+        }
     }
     // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250), so both
     // windows vote on 0 candidates -> -1 for every min_count >= 1 (validated): NA, NA.
     if (lane_id() == 0) {
-        a.out[li] = svt_result{r0, r1};
-        if (COUNT) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(a.out + li);
+        o[w] = r;
+        if (COUNT)
             for (int i = 0; i < 5; i++)
                 if (wk[i]) atomicAdd(a.work + i, wk[i]);
-        }
     }
 }
 
@@ -434,14 +690,17 @@ __global__ __launch_bounds__(64) void refine_kernel(KArgs a) {
 struct svt_ctx {
     svt_params prm{};
     int device = 0;
+    bool stream_gather = true;    // SVTREK_GATHER=perread selects the per-read variant (A/B)
     char err[512] = {0};
     // pileup
     int32_t n_targets = 0;
     int64_t n_reads = 0;
     uint64_t n_ops = 0;
-    int32_t *d_pos = nullptr, *d_emax = nullptr;
+    int32_t *d_pos = nullptr, *d_emax = nullptr, *d_maxspan = nullptr;
     uint4 *d_rec = nullptr;
-    int64_t *d_tid_off = nullptr;
+    uint64_t *d_off64 = nullptr;
+    int64_t *d_tid_off = nullptr, *d_bkt_off = nullptr;
+    uint32_t *d_bkt = nullptr;
     uint32_t *d_cigar = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
@@ -449,7 +708,7 @@ struct svt_ctx {
     svt_locus *d_loci = nullptr;
     svt_result *d_out = nullptr;
     size_t batch_cap = 0;
-    // spill pool + status + work counters (one allocation, memset per call)
+    // spill pool + status + work counters
     int32_t *d_pool = nullptr;
     unsigned long long pool_words = 0;
     unsigned char *d_ctl = nullptr;   // [0,8) pool head, [8,12) status, [16,56) work
@@ -468,15 +727,22 @@ svt_status fail(svt_ctx *c, svt_status code, const char *fmt, const char *detail
         if (e_ != hipSuccess) return fail((ctx), SVT_EDEVICE, #expr ": %s", hipGetErrorString(e_)); \
     } while (0)
 
+template <typename T>
+void hfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
 void free_pileup(svt_ctx *c) {
-    (void)hipFree(c->d_pos); (void)hipFree(c->d_emax); (void)hipFree(c->d_rec); (void)hipFree(c->d_tid_off); (void)hipFree(c->d_cigar);
-    c->d_pos = c->d_emax = nullptr; c->d_rec = nullptr; c->d_tid_off = nullptr; c->d_cigar = nullptr;
+    hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_maxspan); hfree(c->d_rec); hfree(c->d_off64);
+    hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
-    a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_tid_off, c->d_cigar, c->n_targets};
+    a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
+                       c->d_maxspan, c->d_cigar, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
                     c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count};
     a.loci = d_loci;
@@ -492,22 +758,38 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
 
 svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t n, hipStream_t st, bool count) {
     if (n == 0) return SVT_OK;
-    if (n > 0x7fffffffull) return fail(c, SVT_EINVAL, "batch too large (%s)", "n > 2^31-1");
+    if (n > 0x3fffffffull) return fail(c, SVT_EINVAL, "batch too large (%s)", "n > 2^30-1");
     HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 64, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
-    if (count) hipLaunchKernelGGL(refine_kernel<true>, dim3((unsigned)n), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL(refine_kernel<false>, dim3((unsigned)n), dim3(64), 0, st, a);
+    dim3 grid((unsigned)(2 * n)), block(64);
+    if (c->stream_gather) {
+        if (count) hipLaunchKernelGGL((refine_kernel<true, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((refine_kernel<false, true>), grid, block, 0, st, a);
+    } else {
+        if (count) hipLaunchKernelGGL((refine_kernel<true, false>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((refine_kernel<false, false>), grid, block, 0, st, a);
+    }
     HIP_TRY(c, hipGetLastError());
     return SVT_OK;
 }
 
 svt_status ensure_batch(svt_ctx *c, size_t n) {
     if (n <= c->batch_cap) return SVT_OK;
-    (void)hipFree(c->d_loci); (void)hipFree(c->d_out);
-    c->d_loci = nullptr; c->d_out = nullptr; c->batch_cap = 0;
+    hfree(c->d_loci); hfree(c->d_out);
+    c->batch_cap = 0;
     HIP_TRY(c, hipMalloc(&c->d_loci, n * sizeof(svt_locus)));
     HIP_TRY(c, hipMalloc(&c->d_out, n * sizeof(svt_result)));
     c->batch_cap = n;
+    return SVT_OK;
+}
+
+template <typename T>
+svt_status upload(svt_ctx *c, T *&dst, const T *src, size_t n, size_t pad_elems = 0) {
+    size_t bytes = (n + pad_elems) * sizeof(T);
+    HIP_TRY(c, hipMalloc(&dst, bytes ? bytes : sizeof(T)));
+    if (n) HIP_TRY(c, hipMemcpy(dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    if (pad_elems) HIP_TRY(c, hipMemset(dst + n, 0, pad_elems * sizeof(T)));
+    c->dev_bytes += bytes;
     return SVT_OK;
 }
 
@@ -526,6 +808,8 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     svt_ctx *c = new (std::nothrow) svt_ctx();
     if (!c) return SVT_ENOMEM;
     c->prm = *params;
+    const char *g = getenv("SVTREK_GATHER");
+    c->stream_gather = !(g && strcmp(g, "perread") == 0);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;
@@ -540,7 +824,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     uint64_t pool_bytes = params->spill_bytes ? params->spill_bytes : (64ull << 20);
     c->pool_words = pool_bytes / 4;
     if (hipMalloc(&c->d_pool, c->pool_words * 4) != hipSuccess || hipMalloc(&c->d_ctl, 64) != hipSuccess) {
-        (void)hipFree(c->d_pool);
+        hfree(c->d_pool);
         delete c;
         return SVT_ENOMEM;
     }
@@ -565,47 +849,68 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     const uint64_t nops = nr > 0 ? p->cig_off[nr] : 0;
     if (nr > 0 && p->cig_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "cig_off[0] != 0");
 
-    std::vector<int32_t> emax((size_t)nr);
+    std::vector<int32_t> emax((size_t)nr), maxspan((size_t)(nt > 0 ? nt : 1), 0);
     std::vector<uint4> rec((size_t)nr);
+    std::vector<int64_t> bkt_off((size_t)nt + 1, 0);
+    std::vector<uint32_t> bkt;
     for (int32_t t = 0; t < nt; t++) {
-        int32_t m = INT32_MIN;
-        for (int64_t r = p->tid_off[t]; r < p->tid_off[t + 1]; r++) {
-            if (r > p->tid_off[t] && p->pos[r] < p->pos[r - 1])
+        const int64_t r0 = p->tid_off[t], r1 = p->tid_off[t + 1];
+        if (r1 - r0 > 0xffffffffll) return fail(c, SVT_EINVAL, "pileup: %s", "> 2^32 reads on one contig");
+        if (r1 > r0 && p->cig_off[r1] - p->cig_off[r0] >= (1ull << 31))
+            return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^31 CIGAR ops on one contig");
+        int32_t m = INT32_MIN, ms = 0, maxpos = 0;
+        for (int64_t r = r0; r < r1; r++) {
+            if (r > r0 && p->pos[r] < p->pos[r - 1])
                 return fail(c, SVT_EINVAL, "pileup: %s", "reads not sorted by pos within a contig");
             if (p->pos[r] < 0 || p->endpos[r] <= p->pos[r])
                 return fail(c, SVT_EINVAL, "pileup: %s", "pos < 0 or endpos <= pos");
             uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
-            if (o1 < o0 || o1 > nops || o1 - o0 >= (1ull << 30))
-                return fail(c, SVT_EINVAL, "pileup: %s", "bad cig_off");
+            if (o1 < o0 || o1 > nops || o1 - o0 > NCIG_MASK) return fail(c, SVT_EINVAL, "pileup: %s", "bad cig_off");
             uint32_t ncig = (uint32_t)(o1 - o0);
             uint32_t clip;
             if (p->clip) clip = p->clip[r] & 3u;
             else clip = ncig ? (((p->cigar[o1 - 1] & 0xfu) == OP_SOFT ? 1u : 0u) |
                                 ((p->cigar[o0] & 0xfu) == OP_SOFT ? 2u : 0u)) : 0u;
+            // the stream kernel needs every walk position (from pos, or from a dead read's
+            // inter.end+1 start) to stay below 2^32; reads walking >= 2^31 take the exact slow walk
+            uint64_t walk = (uint64_t)(uint32_t)p->pos[r];
+            for (uint64_t i = o0; i < o1; i++) {
+                uint32_t op = p->cigar[i] & 0xfu;
+                if (op != OP_INS && op != OP_SOFT) walk += p->cigar[i] >> 4;
+            }
+            const uint32_t slow = walk >= (1ull << 31) ? SLOW_BIT : 0u;
             if (p->endpos[r] > m) m = p->endpos[r];
+            if (p->endpos[r] - p->pos[r] > ms) ms = p->endpos[r] - p->pos[r];
+            maxpos = std::max(maxpos, p->pos[r]);
             emax[(size_t)r] = m;
-            rec[(size_t)r] = make_uint4((uint32_t)p->endpos[r], ncig | (clip << 30), (uint32_t)o0,
-                                        (uint32_t)(o0 >> 32));
+            rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | slow | (clip << 30),
+                                        (uint32_t)o0);
+        }
+        maxspan[(size_t)t] = ms;
+        // bucket b: first contig-relative read with pos >= b << BKT_SHIFT, b = 0..nb-1
+        const int64_t nb = (r1 > r0 ? ((int64_t)maxpos >> BKT_SHIFT) + 2 : 1) + 1;
+        bkt_off[(size_t)t] = (int64_t)bkt.size();
+        int64_t r = r0;
+        for (int64_t b = 0; b < nb; b++) {
+            while (r < r1 && ((int64_t)p->pos[r] >> BKT_SHIFT) < b) r++;
+            bkt.push_back((uint32_t)(r - r0));
         }
     }
-    size_t nrs = (size_t)(nr > 0 ? nr : 1);
-    HIP_TRY(c, hipMalloc(&c->d_pos, nrs * 4));
-    HIP_TRY(c, hipMalloc(&c->d_emax, nrs * 4));
-    HIP_TRY(c, hipMalloc(&c->d_rec, nrs * 16));
-    HIP_TRY(c, hipMalloc(&c->d_tid_off, (size_t)(nt + 1) * 8));
-    HIP_TRY(c, hipMalloc(&c->d_cigar, (size_t)(nops > 0 ? nops : 1) * 4));
-    if (nr > 0) {
-        HIP_TRY(c, hipMemcpy(c->d_pos, p->pos, (size_t)nr * 4, hipMemcpyHostToDevice));
-        HIP_TRY(c, hipMemcpy(c->d_emax, emax.data(), (size_t)nr * 4, hipMemcpyHostToDevice));
-        HIP_TRY(c, hipMemcpy(c->d_rec, rec.data(), (size_t)nr * 16, hipMemcpyHostToDevice));
-    }
-    if (nt > 0) HIP_TRY(c, hipMemcpy(c->d_tid_off, p->tid_off, (size_t)(nt + 1) * 8, hipMemcpyHostToDevice));
-    else HIP_TRY(c, hipMemset(c->d_tid_off, 0, 8));
-    if (nops > 0) HIP_TRY(c, hipMemcpy(c->d_cigar, p->cigar, nops * 4, hipMemcpyHostToDevice));
+    bkt_off[(size_t)nt] = (int64_t)bkt.size();
+    svt_status s;
+    if ((s = upload(c, c->d_pos, p->pos, (size_t)nr))) return s;
+    if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
+    if ((s = upload(c, c->d_rec, rec.data(), (size_t)nr))) return s;
+    if ((s = upload(c, c->d_off64, p->cig_off, nr > 0 ? (size_t)nr + 1 : 0, nr > 0 ? 0 : 1))) return s;
+    if ((s = upload(c, c->d_maxspan, maxspan.data(), maxspan.size()))) return s;
+    if ((s = upload(c, c->d_bkt, bkt.data(), bkt.size()))) return s;
+    if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
+    if (nt > 0) { if ((s = upload(c, c->d_tid_off, p->tid_off, (size_t)nt + 1))) return s; }
+    else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
+    if ((s = upload(c, c->d_cigar, p->cigar, (size_t)nops, CIGAR_PAD))) return s;
     c->n_targets = nt;
     c->n_reads = nr;
     c->n_ops = nops;
-    c->dev_bytes = (uint64_t)nr * 24 + (uint64_t)(nt + 1) * 8 + nops * 4;
     c->loaded = true;
     return SVT_OK;
 }
@@ -669,7 +974,7 @@ void svt_close(svt_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     free_pileup(c);
-    (void)hipFree(c->d_loci); (void)hipFree(c->d_out); (void)hipFree(c->d_pool); (void)hipFree(c->d_ctl);
+    hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl);
     delete c;
 }
 

@@ -28,8 +28,17 @@ def engine_factory():
 
     engines = []
 
-    def make(params=None):
-        e = Engine(params or Params(), device=0)
+    def make(params=None, gather="stream"):
+        """gather: "stream" (window-stream kernel, default) or "perread" (per-read walk variant)."""
+        old = os.environ.get("SVTREK_GATHER")
+        os.environ["SVTREK_GATHER"] = gather
+        try:
+            e = Engine(params or Params(), device=0)
+        finally:
+            if old is None:
+                os.environ.pop("SVTREK_GATHER", None)
+            else:
+                os.environ["SVTREK_GATHER"] = old
         engines.append(e)
         return e
 

@@ -61,8 +61,9 @@ def test_random_consensus_windows(engine_factory, seed):
     _assert_same(got, want, loci)
 
 
+@pytest.mark.parametrize("gather", ["stream", "perread"])
 @pytest.mark.parametrize("seed", range(10))
-def test_fuzz_pileups(engine_factory, seed):
+def test_fuzz_pileups(engine_factory, seed, gather):
     rng = np.random.default_rng(1000 + seed)
     hot = [int(x) for x in rng.integers(5000, 55000, size=6)]
     pl = random_pileup(rng, n_targets=2, contig_len=60000, n_reads=int(rng.integers(50, 700)),
@@ -70,7 +71,7 @@ def test_fuzz_pileups(engine_factory, seed):
     prm = Params(wider_interval=int(rng.choice([20000, 3000])), median_interval=int(rng.choice([10000, 500])),
                  narrow_interval=int(rng.choice([2000, 100])), consensus_interval_range=int(rng.choice([500, 80])),
                  consensus_interval=int(rng.choice([5, 0, 30])), consensus_min_count=int(rng.choice([1, 2, 3])))
-    eng = engine_factory(prm)
+    eng = engine_factory(prm, gather=gather)
     eng.load_pileup(pl)
     loci = random_loci(rng, 300, 2, 60000, hot)
     got = eng.refine(loci)
@@ -196,3 +197,72 @@ def test_repeatability_and_batch_split(engine_factory):
     assert (b == a[perm]).all()
     c = np.concatenate([eng.refine(r.loci[:123]), eng.refine(r.loci[123:])])
     assert (c == a).all()
+
+
+@pytest.mark.parametrize("gather", ["stream", "perread"])
+def test_hifi_short_cigars(engine_factory, gather):
+    """HiFi-like: ~30 ops per read, many reads per 256-op tile (segment heads mid-lane)."""
+    cfg = sim.SimConfig(seed=12, n_targets=2, n_loci=600, del_frac=0.5, coverage=30, read_len_mean=15000,
+                        read_len_sd=3000, read_len_min=500, rho=1 / 500, spacing=6000, sv_max_len=1500,
+                        p_clip_ends=0.3, p_noise_sv=0.2)
+    r = sim.generate(cfg)
+    eng = engine_factory(gather=gather)
+    eng.load_pileup(r.pileup)
+    got = eng.refine(r.loci)
+    want, ow = O.refine_batch(r.pileup, r.loci, threads=8, with_work=True)
+    _assert_same(got, want, r.loci)
+    w = eng.count_work(r.loci)
+    assert (w["reads"], w["ops_walked"], w["candidates"]) == (ow["reads"], ow["ops_walked"], ow["candidates"])
+
+
+def test_tiny_reads_and_empty_cigars(engine_factory):
+    """1-op and 0-op reads (n_cigar == 0 keeps only the soft-clip tests, with the clip
+    bits ingest recorded from the bytes the reference reads)."""
+    from svtrek_amd.pileup import from_reads
+    rng = np.random.default_rng(5)
+    rows, clip = [], {}
+    for i in range(3000):
+        pos = int(rng.integers(0, 30000))
+        kind = rng.random()
+        if kind < 0.25:
+            ops = []
+            clip[i] = int(rng.integers(0, 4))
+        elif kind < 0.6:
+            ops = [(int(rng.choice([0, 2, 4, 1, 5])), int(rng.choice([1, 3, 51, 60, 120])))]
+        else:
+            ops = [(int(rng.choice([0, 2, 4, 1, 8, 3])), int(rng.choice([1, 2, 51, 300]))) for _ in range(int(rng.integers(2, 9)))]
+        rows.append((0, pos, ops))
+    pl = from_reads(1, rows, clip=clip)
+    for gather in ("stream", "perread"):
+        eng = engine_factory(Params(consensus_min_count=1), gather=gather)
+        eng.load_pileup(pl)
+        loci = make_loci([(int(rng.choice([1, 2])), 1, int(p), int(p) + int(d)) for p, d in
+                          zip(rng.integers(0, 32000, 400), rng.integers(51, 3000, 400))])
+        got = eng.refine(loci)
+        want = O.refine_batch(pl, loci, Params(consensus_min_count=1))
+        _assert_same(got, want, loci)
+
+
+def test_wrapping_walks_take_exact_path(engine_factory):
+    """Reads whose walk position passes 2^31 (huge H/P/N ops advance rp, refinement.c:141)
+    and windows ending past 2^31: exact uint32 replay, same as the oracle."""
+    from svtrek_amd.pileup import from_reads
+    big = (1 << 28) - 1
+    rows = []
+    for i in range(200):
+        pos = 10000 + 37 * i
+        ops = [(0, 500), (2, 80), (0, 300)]
+        if i % 3 == 0:
+            ops += [(5, big)] * 9 + [(2, 70), (0, 10)]
+        if i % 5 == 0:
+            ops = [(4, 20)] + ops + [(4, 30)]
+        rows.append((0, pos, ops))
+    pl = from_reads(1, rows)
+    loci = make_loci([(2, 1, 10000 + 500 + 37 * k, 10000 + 580 + 37 * k) for k in range(0, 200, 7)] +
+                     [(2, 1, (1 << 31) - 1000, (1 << 31) + 5000), (1, 1, 10600, 10601)])
+    for gather in ("stream", "perread"):
+        eng = engine_factory(gather=gather)
+        eng.load_pileup(pl)
+        got = eng.refine(loci)
+        want = O.refine_batch(pl, loci)
+        _assert_same(got, want, loci)
