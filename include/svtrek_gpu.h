@@ -146,7 +146,7 @@ void        svt_close(svt_ctx *ctx);
 const char *svt_version(void);
 
 /* LDS candidate capacity per window; larger windows spill to the device pool. */
-#define SVT_LDS_CANDS 512
+#define SVT_LDS_CANDS 256
 
 #ifdef __cplusplus
 }

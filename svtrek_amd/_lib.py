@@ -22,7 +22,7 @@ STATUS_NAMES = {0: "OK", -1: "EINVAL", -2: "EDEVICE", -3: "ENOMEM", -4: "ESTATE"
 
 SVT_UNKNOWN, SVT_INS, SVT_DEL, SVT_INV, SVT_DUP, SVT_TRA, SVT_BND = range(7)
 SVT_NA = 0xFFFFFFFF
-SVT_LDS_CANDS = 512
+SVT_LDS_CANDS = 256
 
 LOCUS_DTYPE = np.dtype([("type", "<i4"), ("chrom", "<i4"), ("pos", "<u4"), ("end", "<u4")])
 RESULT_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4")])

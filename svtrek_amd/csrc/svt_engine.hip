@@ -7,14 +7,13 @@
 //      bucket index (first read per 4 kb of contig) + one 64-lane probe each for the
 //      sorted pos[] and the prefix-max-of-endpos emax[] arrays;
 //   2. streams the window's CIGAR words -- the reads [lo, hi) own ONE contiguous span
-//      of the CIGAR arena -- in 256-op tiles, one 16-B load per lane (1 KiB per wave
-//      instruction, fully coalesced, next tile prefetched while the current one is
-//      voted on).  A segmented wave prefix scan (DPP) of the reference advance, reset at
+//      of the CIGAR arena -- in 1024-op tiles, four 16-B loads per lane (4 KiB per wave,
+//      fully coalesced, next tile prefetched while the current one is processed).  A segmented wave prefix scan (DPP) of the reference advance, reset at
 //      each read's first op to its pos, gives every op's walk position at once; because
 //      the walk position only grows inside a read, "this op comes after the break of
 //      refinement.c:145-148" is just `position before the op > inter.end`, so no second
 //      scan is needed.  Breakpoint candidates (A4-A6) and the soft-clip candidates of
-//      each read's stop op are compacted into LDS with ballots; tails of reads that
+//      each read's stop op are appended to LDS with LDS atomics; tails of reads that
 //      already broke (and reads that do not overlap the window) are skipped;
 //   3. bitonic-sorts the candidates in LDS and runs consensus_pos's asymmetric vote
 //      (A8-A10): per-element cluster counts in parallel (binary search + int64 prefix
@@ -36,12 +35,11 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.2.0 (gfx950, window-stream kernel)"
+#define SVT_VERSION "svtrek_amd 0.3.0 (gfx950, window-stream kernel)"
 
 namespace {
 
 constexpr int WAVE = 64;
-constexpr int TILE = 256;                   // CIGAR ops per stream step (4 per lane)
 constexpr int CAP = SVT_LDS_CANDS;          // LDS candidates per window
 constexpr int SV_MIN_LENGTH = 50;           // params.h:33
 constexpr uint32_t OP_INS = 1, OP_DEL = 2, OP_SOFT = 4;   // params.h:11-14
@@ -50,7 +48,7 @@ constexpr int32_t T_INS = 1, T_DEL = 2;
 constexpr int BKT_SHIFT = 12;               // read-start bucket = 4096 bp
 constexpr uint32_t NCIG_MASK = 0x1fffffffu; // rec.z: n_cigar | slow << 29 | clip << 30
 constexpr uint32_t SLOW_BIT = 1u << 29;
-constexpr uint32_t CIGAR_PAD = 260;         // zero words after the arena (tile over-read)
+constexpr uint32_t CIGAR_PAD = 1040;        // zero words after the arena (tile over-read)
 
 struct DevPileup {
     const int32_t *pos;       // [n_reads]
@@ -171,16 +169,19 @@ __device__ __forceinline__ int64_t wave_partition_point(int64_t l, int64_t h, Pr
 }
 
 // ------------------------------------------------------------------ candidate sink
+// Candidates are appended with LDS atomics: their order is irrelevant (the multiset is
+// sorted before the vote) and they are rare next to the CIGAR ops streamed, so a lane
+// that finds one appends it on its own, under any divergence.
 struct Sink {
     int32_t *buf;   // LDS or a global spill slab
     int32_t cap;
-    int32_t n;      // total candidates seen (may exceed cap: then a spill re-run follows)
+    int32_t *cnt;   // LDS counter: candidates seen (may exceed cap -> spill re-run)
+    __device__ __forceinline__ void push1(int32_t val) {
+        int idx = atomicAdd(cnt, 1);
+        if (idx < cap) buf[idx] = val;
+    }
     __device__ __forceinline__ void push(bool pred, int32_t val) {
-        uint64_t m = ballot(pred);
-        if (!m) return;
-        int idx = n + __popcll(m & ((1ull << lane_id()) - 1ull));
-        if (pred && idx < cap) buf[idx] = val;
-        n += __popcll(m);
+        if (pred) push1(val);
     }
 };
 
@@ -272,10 +273,10 @@ __device__ __forceinline__ bool read_range(const DevPileup &P, int tid, int64_t 
 
 // ------------------------------------------------------------------ per-read gather (v1)
 template <int KIND, bool COUNT>
-__device__ __forceinline__ int32_t gather_perread(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st) {
+__device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi)) return sink.n;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
     const int ln = lane_id();
     for (int64_t base = lo; base < hi; base += WAVE) {
         int64_t r = base + ln;
@@ -291,29 +292,34 @@ __device__ __forceinline__ int32_t gather_perread(const DevPileup &P, int tid, u
                                    st);
         }
     }
-    return sink.n;
 }
 
-// ------------------------------------------------------------------ window stream (v2)
+// ------------------------------------------------------------------ window stream
+constexpr int OPL = 8;                      // CIGAR ops per lane per tile
+constexpr int TILE = OPL * WAVE;            // 512 ops (2 KiB) per stream step
+
 struct StreamLds {
-    int8_t head[TILE + 8];   // per tile op: block-relative read index of a read's first op, else -1
+    alignas(16) int8_t head[TILE + 8];   // per tile op: block-relative index of the read starting there, else -1
+    uint32_t hrp[WAVE];                   // read k's walk start: pos, or inter.end+1 when it yields nothing
+    uint32_t rpos[WAVE];
+    uint32_t clip[WAVE];
 };
 
 template <int KIND, bool COUNT>
-__device__ __forceinline__ int32_t gather_stream(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
-                                 StreamLds &L) {
+__device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
+                                              WinStats &st, StreamLds &L) {
     // Positions in the stream stay below 2^32 (no wrap) when inter.end < 2^31 and every
     // streamed read walks less than 2^31 (the others are flagged slow at load time).
-    if (e >= 0x80000000u) return gather_perread<KIND, COUNT>(P, tid, s, e, sink, st);
+    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi)) return sink.n;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
     const int ln = lane_id();
     const uint64_t S0 = P.off64[lo];
     const uint32_t base32 = (uint32_t)S0;
     const uint32_t *cg = P.cigar;
-    const uint32_t dead_rp = e + 1u;   // stream start position of reads that yield nothing
-    int32_t *hw = reinterpret_cast<int32_t *>(L.head);
+    const uint32_t dead_rp = e + 1u;   // walk start of reads that yield nothing: every op is past the break
+    uint32_t live_ops = 0;             // COUNT builds
 
     for (int64_t rb = lo; rb < hi; rb += WAVE) {
         // ---- one block of up to 64 reads, lane k <-> read rb + k
@@ -326,10 +332,13 @@ __device__ __forceinline__ int32_t gather_stream(const DevPileup &P, int tid, ui
         const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op
         const int32_t en0 = st0 + (int32_t)ncig;
         const bool live = ovl && !slow && ncig > 0;
-        const uint32_t hrp = live ? rpos : dead_rp;                 // segment start of this read's walk
+        const bool has_ops = inb && ncig > 0;
         const int nblk = (int)min<int64_t>(WAVE, hi - rb);
         const int32_t blk_end = rdlane_i(en0, nblk - 1);
-        const bool has_ops = inb && ncig > 0;
+        __syncthreads();
+        L.hrp[ln] = live ? rpos : dead_rp;
+        L.rpos[ln] = rpos;
+        L.clip[ln] = clip;
 
         // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
         if (KIND != K_INS) {
@@ -346,62 +355,70 @@ __device__ __forceinline__ int32_t gather_stream(const DevPileup &P, int tid, ui
         int32_t J = live_m ? rdlane_i(st0, __builtin_ctzll(live_m)) : blk_end;
         uint32_t carry_rp = 0;
         int32_t carry_k = -1;
-        uint4 wcur = make_uint4(0, 0, 0, 0);
         int32_t A = 0;
+        uint4 cw[OPL / 4];
+#pragma unroll
+        for (int q = 0; q < OPL / 4; q++) cw[q] = make_uint4(0, 0, 0, 0);
         if (J < blk_end) {
             A = (int32_t)(((S0 + (uint64_t)(int64_t)J) & ~3ull) - S0);
-            wcur = *reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)A + 4 * ln);
+            const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)A + OPL * ln);
+#pragma unroll
+            for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
         }
         while (J < blk_end) {
             const int32_t U = min(A + TILE, blk_end);
-            // ---- head table: which ops start a read
-            hw[ln] = -1;
-            if (ln == 0) hw[WAVE] = -1;
+            // ---- head table: the ops that start a read
+            reinterpret_cast<int2 *>(L.head)[ln] = make_int2(-1, -1);
+            if (ln == 0) reinterpret_cast<int2 *>(L.head)[WAVE] = make_int2(-1, -1);
             __syncthreads();
             if (has_ops && st0 >= A && st0 <= A + TILE) L.head[st0 - A] = (int8_t)ln;
             __syncthreads();
-            const int32_t hword = hw[ln];
-            const int32_t hnext = ln == WAVE - 1 ? (int32_t)L.head[TILE] : 0;
-            int32_t hk[4];
+            const int2 hq = reinterpret_cast<const int2 *>(L.head)[ln];
+            const int32_t h_after = (int32_t)L.head[TILE];   // op right after the tile (lane 63's last op + 1)
+            const uint32_t hw[2] = {(uint32_t)hq.x, (uint32_t)hq.y};
+            uint32_t wv[OPL];
 #pragma unroll
-            for (int i = 0; i < 4; i++) hk[i] = (int32_t)(int8_t)(hword >> (8 * i));
-            const int32_t nexth0 = __shfl_down(hk[0], 1, WAVE);
-            const uint32_t wv[4] = {wcur.x, wcur.y, wcur.z, wcur.w};
-
-            // ---- local (4 ops) segmented inclusive scan of the reference advance
-            uint32_t op[4], len[4], adv[4], lv[4], lh[4];
-            bool valid[4];
-            uint32_t H = 0, V = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int32_t j = A + 4 * ln + i;
-                valid[i] = j >= J && j < U;
-                op[i] = wv[i] & 0xfu;
-                len[i] = wv[i] >> 4;
-                adv[i] = (valid[i] && op[i] != OP_INS && op[i] != OP_SOFT) ? len[i] : 0u;   // refinement.c:141
-                const bool ishead = valid[i] && hk[i] >= 0;
-                const uint32_t h0 = __shfl(hrp, hk[i] < 0 ? 0 : hk[i], WAVE);
-                if (ishead) { H = 1; V = h0 + adv[i]; }
-                else V += adv[i];
-                lv[i] = V;
-                lh[i] = H;
+            for (int q = 0; q < OPL / 4; q++) {
+                wv[4 * q] = cw[q].x; wv[4 * q + 1] = cw[q].y; wv[4 * q + 2] = cw[q].z; wv[4 * q + 3] = cw[q].w;
             }
-            // ---- wave segmented scan over the lane aggregates, then exclusive per lane
-            uint32_t Hi = H, Vi = V;
+            const int32_t jb = A + OPL * ln;                  // this lane's first op
+            const int32_t vlo = min(max(J - jb, 0), OPL), vhi = min(max(U - jb, 0), OPL);
+            const uint32_t vmask = ((1u << vhi) - 1u) & ~((1u << vlo) - 1u);
+
+            // ---- pass 1: lane-local segmented inclusive scan of the reference advance
+            uint32_t adv[OPL], lv[OPL];
+            uint32_t V = 0, hmask = 0, rawh = 0, cmask = 0;
+            int32_t kmax = -1;
+#pragma unroll
+            for (int i = 0; i < OPL; i++) {
+                const uint32_t vi = (vmask >> i) & 1u;
+                const uint32_t op = wv[i] & 0xfu, len = wv[i] >> 4;
+                const uint32_t keep = vi & (uint32_t)(op != OP_INS) & (uint32_t)(op != OP_SOFT);   // refinement.c:141
+                adv[i] = len & (0u - keep);
+                const int32_t hb = (int32_t)(int8_t)(hw[i >> 2] >> (8 * (i & 3)));
+                const uint32_t rh = (uint32_t)(hb >= 0);
+                const uint32_t hd = vi & rh;
+                const uint32_t hv = L.hrp[hb & (WAVE - 1)];
+                V = hd ? hv + adv[i] : V + adv[i];
+                lv[i] = V;
+                rawh |= rh << i;
+                hmask |= hd << i;
+                kmax = hd ? hb : kmax;
+                cmask |= (vi & (uint32_t)is_candidate_op<KIND>(op, len)) << i;
+            }
+            // ---- wave: segmented scan of lane aggregates -> position before each lane
+            uint32_t Hi = hmask != 0, Vi = V;
             wave_seg_scan(Hi, Vi);
-            const uint32_t Hx = dpp<0x138, 0xf>(Hi), Vx = dpp<0x138, 0xf>(Vi);
+            const uint32_t Hx = dpp<0x138, 0xf>(Hi), Vx = dpp<0x138, 0xf>(Vi);   // wave_shr:1
             const uint32_t pre = Hx ? Vx : carry_rp + Vx;
             const uint32_t H63 = rdlane(Hi, WAVE - 1), V63 = rdlane(Vi, WAVE - 1);
             const uint32_t next_carry_rp = H63 ? V63 : carry_rp + V63;
-            // read index of every op (max scan of the head table)
-            int32_t km = -1, kl[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) { km = max(km, valid[i] ? hk[i] : -1); kl[i] = km; }
-            const int32_t kinc = wave_scan_max(km);
+            const int32_t kinc = wave_scan_max(kmax);
             const int32_t kex = dpp_i<0x138, 0xf>(kinc, -1);
             const int32_t next_carry_k = max(carry_k, rdlane_i(kinc, WAVE - 1));
 
-            // ---- next tile: continue the read at U unless it already broke / yields nothing
+            // ---- next tile: continue the read at U unless it already broke / yields nothing;
+            //      otherwise jump to the next read that yields.  Prefetch it now.
             int32_t Jn = U;
             {
                 const int32_t kc = next_carry_k;
@@ -412,50 +429,52 @@ __device__ __forceinline__ int32_t gather_stream(const DevPileup &P, int tid, ui
                 }
             }
             int32_t An = A;
-            uint4 wnext = wcur;
-            if (Jn < blk_end) {   // prefetch while this tile is voted on
+            if (Jn < blk_end) {   // cw is dead after wv was unpacked: reuse it for the prefetch
                 An = (int32_t)(((S0 + (uint64_t)(int64_t)Jn) & ~3ull) - S0);
-                wnext = *reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)An + 4 * ln);
+                const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)An + OPL * ln);
+#pragma unroll
+                for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
             }
 
-            // ---- per op: walk position after / before, break, candidates, stop ops
-            unsigned long long live_ops = 0;
+            // ---- pass 2: walk positions, break, candidates, stop ops
+            const uint32_t nh = dpp<0x130, 0xf>(rawh) & 1u;                   // wave_shl:1: next lane's op 0
+            const uint32_t next_head = ln == WAVE - 1 ? (uint32_t)(h_after >= 0) : nh;
+            const uint32_t lastm = (rawh >> 1) | (next_head << (OPL - 1));    // bit i: op i+1 starts a read
+            int32_t k = max(carry_k, kex);
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t after = lh[i] ? lv[i] : pre + lv[i];
+            for (int i = 0; i < OPL; i++) {
+                const uint32_t vi = (vmask >> i) & 1u;
+                const uint32_t anyh = hmask & ((2u << i) - 1u);
+                const uint32_t after = anyh ? lv[i] : pre + lv[i];
                 const uint32_t before = after - adv[i];
-                const bool lv_op = valid[i] && before <= e;    // not past this read's break
-                const bool brk = lv_op && after > e;           // the break op itself (refinement.c:145)
-                sink.push(lv_op && is_candidate_op<KIND>(op[i], len[i]),
-                          KIND == K_END ? (int32_t)(before + len[i] + 1u) : (int32_t)before);   // :198 / :136
-                if (COUNT) live_ops += (unsigned long long)__popcll(ballot(lv_op));
+                const bool lvop = vi && before <= e;          // not past this read's break
+                const bool brk = lvop && after > e;           // the break op itself (refinement.c:145)
+                const int32_t hb = (int32_t)(int8_t)(hw[i >> 2] >> (8 * (i & 3)));
+                k = ((hmask >> i) & 1u) ? hb : k;
+                if (COUNT) live_ops += lvop ? 1u : 0u;
+                if (lvop && ((cmask >> i) & 1u)) {
+                    const uint32_t len = wv[i] >> 4;
+                    sink.push1(KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before);   // :198 / :136
+                }
                 if (KIND != K_INS) {
-                    const int32_t j = A + 4 * ln + i;
-                    const int32_t hn = i < 3 ? hk[i + 1] : (ln == WAVE - 1 ? hnext : nexth0);
-                    const bool is_last = valid[i] && (j + 1 == blk_end || (j + 1 < A + TILE + 1 && hn >= 0));
-                    const bool stop = brk || (lv_op && is_last);
-                    if (ballot(stop)) {
-                        const int32_t k = max(max(carry_k, kex), kl[i]);
-                        const int32_t kk = k < 0 ? 0 : k;
-                        const uint32_t kclip = (uint32_t)__shfl((int)clip, kk, WAVE);
-                        const uint32_t kpos = (uint32_t)__shfl((int)rpos, kk, WAVE);
-                        if (KIND == K_START)   // trailing S, no break, s <= rp <= e  (refinement.c:152)
-                            sink.push(stop && !brk && (kclip & SVT_CLIP_LAST_S) && s <= after && after <= e,
-                                      (int32_t)after);
-                        else                   // leading S and s <= pos <= e: push rp + 1  (:210-220)
-                            sink.push(stop && (kclip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)kpos &&
-                                          (int64_t)kpos <= (int64_t)e,
-                                      (int32_t)(after + 1u));
-                        if (COUNT && KIND == K_START) live_ops += (unsigned long long)__popcll(ballot(brk && !is_last));
+                    const bool is_last = vi && (jb + i + 1 == blk_end || ((lastm >> i) & 1u));
+                    if (brk || (lvop && is_last)) {           // this read's walk stops here
+                        const uint32_t kc = L.clip[k];
+                        if (KIND == K_START) {                // trailing S, no break, s <= rp <= e (:152)
+                            if (!brk && (kc & SVT_CLIP_LAST_S) && s <= after && after <= e) sink.push1((int32_t)after);
+                            if (COUNT && brk && !is_last) live_ops++;   // cigar[n-1] test word
+                        } else {                              // leading S and s <= pos <= e: rp + 1 (:210-220)
+                            const uint32_t kp = L.rpos[k];
+                            if ((kc & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)kp && (int64_t)kp <= (int64_t)e)
+                                sink.push1((int32_t)(after + 1u));
+                        }
                     }
                 }
             }
-            if (COUNT) st.ops += live_ops;
             carry_rp = next_carry_rp;
             carry_k = next_carry_k;
             J = Jn;
             A = An;
-            wcur = wnext;
         }
         // reads whose walk could wrap uint32: exact per-read replay
         uint64_t sm = ballot(ovl && slow);
@@ -466,7 +485,7 @@ __device__ __forceinline__ int32_t gather_stream(const DevPileup &P, int tid, ui
                                    rdlane(clip, l), s, e, sink, st);
         }
     }
-    return sink.n;
+    if (COUNT) st.ops += rdlane(wave_scan_add(live_ops), WAVE - 1);
 }
 
 // ------------------------------------------------------------------ sort + vote (A8-A10)
@@ -599,32 +618,36 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
 }
 
 struct WinLds {
+    union {                       // the stream scratch is dead once the vote starts
+        StreamLds sl;
+        int64_t pre[CAP + 1];
+    };
     int32_t cand[CAP];
-    int64_t pre[CAP + 1];
-    StreamLds sl;
+    int32_t ncand;
 };
 
 template <int KIND, bool COUNT, bool STREAM>
 __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
                                           StreamLds &L) {
-    if (STREAM) return gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L);
-    return gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    if (lane_id() == 0) *sink.cnt = 0;
+    __syncthreads();
+    if (STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L);
+    else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    __syncthreads();
+    return uniform_i(*sink.cnt);
 }
 
 template <int KIND, bool COUNT, bool STREAM>
 __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e, uint32_t imprecise,
                                  unsigned long long *wk) {
     WinStats st;
-    Sink sink{lds.cand, CAP, 0};
+    Sink sink{lds.cand, CAP, &lds.ncand};
     int32_t n = gather<KIND, COUNT, STREAM>(a, chrom - 1, s, e, sink, st, lds.sl);
     if (COUNT && lane_id() == 0) {
         wk[0] += 1; wk[1] += st.reads; wk[2] += st.ops; wk[3] += (unsigned long long)n;
     }
     if (n < a.prm.min_count) return -1;                    // refinement.c:43-45
-    if (n <= CAP) {
-        __syncthreads();
-        return sort_and_vote(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm);
-    }
+    if (n <= CAP) return sort_and_vote(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm);
     // spill: a slab for N ints + (n+1) int64 from the device pool, then re-gather into it
     if (COUNT && lane_id() == 0) wk[4] += 1;
     int N = 1;
@@ -640,9 +663,8 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     int32_t *g = a.pool + base;
     int64_t *gp = (int64_t *)(a.pool + ((base + (unsigned long long)N + 1ull) & ~1ull));
     WinStats st2;
-    Sink s2{g, N, 0};
+    Sink s2{g, N, &lds.ncand};
     gather<KIND, false, STREAM>(a, chrom - 1, s, e, s2, st2, lds.sl);
-    __syncthreads();
     return sort_and_vote(g, gp, n, (int32_t)imprecise, a.prm);
 }
 

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Run ON THE GPU BOX: GPU parity tests, then bench (stream + perread gather variants).
+# Stops at the first step that crashes / times out; a plain test failure (rc 1) still
+# lets the benches run so one call yields both signals.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+TAG=${1:-check}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+run() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] start $name" >> "$OUT/steps.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] end $name rc=$rc" >> "$OUT/steps.log"
+  return $rc
+}
+run pytest 600 python -m pytest tests -m gpu -x -q; rc=$?
+tail -5 "$OUT/pytest.log"
+if [ $rc -gt 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
+run bench_stream 300 python bench.py --steps 20 --warmup 3 || exit $?
+tail -1 "$OUT/bench_stream.log"
+SVTREK_GATHER=perread run bench_perread 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
+tail -1 "$OUT/bench_perread.log"
+exit $rc
