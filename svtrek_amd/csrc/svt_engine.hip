@@ -35,7 +35,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.3.0 (gfx950, window-stream kernel)"
+#define SVT_VERSION "svtrek_amd 0.4.0 (gfx950, window-stream kernel)"
 
 namespace {
 
@@ -295,14 +295,16 @@ __device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint
 }
 
 // ------------------------------------------------------------------ window stream
+// HBM layout (svt_load_pileup): every read's CIGAR starts on a multiple of OPL words and
+// is padded with zero words (0M: advances nothing, never a candidate) to the next
+// multiple, so each lane's OPL ops of a tile belong to exactly one read.
 constexpr int OPL = 8;                      // CIGAR ops per lane per tile
 constexpr int TILE = OPL * WAVE;            // 512 ops (2 KiB) per stream step
 
 struct StreamLds {
-    alignas(16) int8_t head[TILE + 8];   // per tile op: block-relative index of the read starting there, else -1
-    uint32_t hrp[WAVE];                   // read k's walk start: pos, or inter.end+1 when it yields nothing
-    uint32_t rpos[WAVE];
-    uint32_t clip[WAVE];
+    int8_t slot[WAVE + 4];   // per tile lane slot: block-relative index of the read starting there, else -1
+    uint2 walk[WAVE];        // read k: {walk start (pos, or inter.end+1 when it yields nothing), real op end}
+    uint2 meta[WAVE];        // read k: {pos, clip bits}
 };
 
 template <int KIND, bool COUNT>
@@ -329,16 +331,14 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
         const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
         const bool slow = (rc.z & SLOW_BIT) != 0;
         const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
-        const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op
-        const int32_t en0 = st0 + (int32_t)ncig;
+        const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op (multiple of OPL)
+        const int32_t en_pad = st0 + (int32_t)((ncig + (OPL - 1)) & ~(uint32_t)(OPL - 1));
         const bool live = ovl && !slow && ncig > 0;
-        const bool has_ops = inb && ncig > 0;
         const int nblk = (int)min<int64_t>(WAVE, hi - rb);
-        const int32_t blk_end = rdlane_i(en0, nblk - 1);
+        const int32_t blk_end = rdlane_i(en_pad, nblk - 1);
         __syncthreads();
-        L.hrp[ln] = live ? rpos : dead_rp;
-        L.rpos[ln] = rpos;
-        L.clip[ln] = clip;
+        L.walk[ln] = make_uint2(live ? rpos : dead_rp, (uint32_t)(st0 + (int32_t)ncig));
+        L.meta[ln] = make_uint2(rpos, clip);
 
         // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
         if (KIND != K_INS) {
@@ -355,66 +355,54 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
         int32_t J = live_m ? rdlane_i(st0, __builtin_ctzll(live_m)) : blk_end;
         uint32_t carry_rp = 0;
         int32_t carry_k = -1;
-        int32_t A = 0;
         uint4 cw[OPL / 4];
 #pragma unroll
         for (int q = 0; q < OPL / 4; q++) cw[q] = make_uint4(0, 0, 0, 0);
         if (J < blk_end) {
-            A = (int32_t)(((S0 + (uint64_t)(int64_t)J) & ~3ull) - S0);
-            const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)A + OPL * ln);
+            const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)J + OPL * ln);
 #pragma unroll
             for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
         }
         while (J < blk_end) {
+            const int32_t A = J;                             // tiles start on a read start or a tile end
             const int32_t U = min(A + TILE, blk_end);
-            // ---- head table: the ops that start a read
-            reinterpret_cast<int2 *>(L.head)[ln] = make_int2(-1, -1);
-            if (ln == 0) reinterpret_cast<int2 *>(L.head)[WAVE] = make_int2(-1, -1);
+            const int32_t jb = A + OPL * ln;                 // this lane's first op
+            const bool lane_ok = jb < U;
+            // ---- which lanes start a read
+            L.slot[ln] = -1;
+            if (ln == 0) L.slot[WAVE] = -1;
             __syncthreads();
-            if (has_ops && st0 >= A && st0 <= A + TILE) L.head[st0 - A] = (int8_t)ln;
+            if (ncig > 0 && inb && st0 >= A && st0 <= A + TILE) L.slot[(st0 - A) / OPL] = (int8_t)ln;
             __syncthreads();
-            const int2 hq = reinterpret_cast<const int2 *>(L.head)[ln];
-            const int32_t h_after = (int32_t)L.head[TILE];   // op right after the tile (lane 63's last op + 1)
-            const uint32_t hw[2] = {(uint32_t)hq.x, (uint32_t)hq.y};
+            const int32_t hk = lane_ok ? (int32_t)L.slot[ln] : -1;
+            const int32_t kinc = wave_scan_max(hk);
+            const int32_t kl = max(carry_k, kinc);           // this lane's read
+            const uint2 wk = L.walk[kl < 0 ? 0 : kl];       // {walk start, real end}
+
+            // ---- per op: reference advance and its running sum inside the lane
             uint32_t wv[OPL];
 #pragma unroll
             for (int q = 0; q < OPL / 4; q++) {
                 wv[4 * q] = cw[q].x; wv[4 * q + 1] = cw[q].y; wv[4 * q + 2] = cw[q].z; wv[4 * q + 3] = cw[q].w;
             }
-            const int32_t jb = A + OPL * ln;                  // this lane's first op
-            const int32_t vlo = min(max(J - jb, 0), OPL), vhi = min(max(U - jb, 0), OPL);
-            const uint32_t vmask = ((1u << vhi) - 1u) & ~((1u << vlo) - 1u);
-
-            // ---- pass 1: lane-local segmented inclusive scan of the reference advance
-            uint32_t adv[OPL], lv[OPL];
-            uint32_t V = 0, hmask = 0, rawh = 0, cmask = 0;
-            int32_t kmax = -1;
+            uint32_t Pi[OPL], T = 0, candm = 0;
 #pragma unroll
             for (int i = 0; i < OPL; i++) {
-                const uint32_t vi = (vmask >> i) & 1u;
                 const uint32_t op = wv[i] & 0xfu, len = wv[i] >> 4;
-                const uint32_t keep = vi & (uint32_t)(op != OP_INS) & (uint32_t)(op != OP_SOFT);   // refinement.c:141
-                adv[i] = len & (0u - keep);
-                const int32_t hb = (int32_t)(int8_t)(hw[i >> 2] >> (8 * (i & 3)));
-                const uint32_t rh = (uint32_t)(hb >= 0);
-                const uint32_t hd = vi & rh;
-                const uint32_t hv = L.hrp[hb & (WAVE - 1)];
-                V = hd ? hv + adv[i] : V + adv[i];
-                lv[i] = V;
-                rawh |= rh << i;
-                hmask |= hd << i;
-                kmax = hd ? hb : kmax;
-                cmask |= (vi & (uint32_t)is_candidate_op<KIND>(op, len)) << i;
+                const uint32_t keep = ((0x12u >> op) & 1u) ^ 1u;   // op not in {I, S}: refinement.c:141
+                T += len & (0u - keep);
+                Pi[i] = T;
+                candm |= (uint32_t)is_candidate_op<KIND>(op, len) << i;
             }
-            // ---- wave: segmented scan of lane aggregates -> position before each lane
-            uint32_t Hi = hmask != 0, Vi = V;
+            if (!lane_ok) { T = 0; candm = 0; }
+            // ---- wave: segmented scan of lane sums -> walk position before each lane
+            const uint32_t H = hk >= 0;
+            uint32_t Hi = H, Vi = H ? wk.x + T : T;
             wave_seg_scan(Hi, Vi);
             const uint32_t Hx = dpp<0x138, 0xf>(Hi), Vx = dpp<0x138, 0xf>(Vi);   // wave_shr:1
-            const uint32_t pre = Hx ? Vx : carry_rp + Vx;
+            const uint32_t pre = H ? wk.x : (Hx ? Vx : carry_rp + Vx);
             const uint32_t H63 = rdlane(Hi, WAVE - 1), V63 = rdlane(Vi, WAVE - 1);
             const uint32_t next_carry_rp = H63 ? V63 : carry_rp + V63;
-            const int32_t kinc = wave_scan_max(kmax);
-            const int32_t kex = dpp_i<0x138, 0xf>(kinc, -1);
             const int32_t next_carry_k = max(carry_k, rdlane_i(kinc, WAVE - 1));
 
             // ---- next tile: continue the read at U unless it already broke / yields nothing;
@@ -422,59 +410,59 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
             int32_t Jn = U;
             {
                 const int32_t kc = next_carry_k;
-                const bool cont = kc >= 0 && U < rdlane_i(en0, kc);
+                const bool cont = kc >= 0 && U < rdlane_i(en_pad, kc);
                 if (!(cont && next_carry_rp <= e)) {
                     const uint64_t later = kc >= 0 ? (live_m & ~((2ull << kc) - 1ull)) : live_m;
                     Jn = later ? max(U, rdlane_i(st0, __builtin_ctzll(later))) : blk_end;
                 }
             }
-            int32_t An = A;
-            if (Jn < blk_end) {   // cw is dead after wv was unpacked: reuse it for the prefetch
-                An = (int32_t)(((S0 + (uint64_t)(int64_t)Jn) & ~3ull) - S0);
-                const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)An + OPL * ln);
+            if (Jn < blk_end) {   // cw is dead once wv is unpacked: reuse it for the prefetch
+                const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)Jn + OPL * ln);
 #pragma unroll
                 for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
             }
 
-            // ---- pass 2: walk positions, break, candidates, stop ops
-            const uint32_t nh = dpp<0x130, 0xf>(rawh) & 1u;                   // wave_shl:1: next lane's op 0
-            const uint32_t next_head = ln == WAVE - 1 ? (uint32_t)(h_after >= 0) : nh;
-            const uint32_t lastm = (rawh >> 1) | (next_head << (OPL - 1));    // bit i: op i+1 starts a read
-            int32_t k = max(carry_k, kex);
+            // ---- walk positions: ops [0, nb) end at or before inter.end, op nb is the break
+            //      (refinement.c:145) when nb < OPL; positions only grow inside a read.
+            const bool lane_live = lane_ok && pre <= e;      // not past this read's break
+            uint32_t nb = 0;
 #pragma unroll
-            for (int i = 0; i < OPL; i++) {
-                const uint32_t vi = (vmask >> i) & 1u;
-                const uint32_t anyh = hmask & ((2u << i) - 1u);
-                const uint32_t after = anyh ? lv[i] : pre + lv[i];
-                const uint32_t before = after - adv[i];
-                const bool lvop = vi && before <= e;          // not past this read's break
-                const bool brk = lvop && after > e;           // the break op itself (refinement.c:145)
-                const int32_t hb = (int32_t)(int8_t)(hw[i >> 2] >> (8 * (i & 3)));
-                k = ((hmask >> i) & 1u) ? hb : k;
-                if (COUNT) live_ops += lvop ? 1u : 0u;
-                if (lvop && ((cmask >> i) & 1u)) {
-                    const uint32_t len = wv[i] >> 4;
-                    sink.push1(KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before);   // :198 / :136
+            for (int i = 0; i < OPL; i++) nb += (pre + Pi[i] <= e) ? 1u : 0u;
+            const int32_t nreal = min(max((int32_t)wk.y - jb, 0), OPL);   // real (unpadded) ops here
+            const uint32_t livem = lane_live ? ((2u << nb) - 1u) & ((1u << OPL) - 1u) : 0u;
+            const bool brk = lane_live && (int32_t)nb < nreal;             // this lane holds the break op
+            const int32_t lr = (int32_t)wk.y - 1 - jb;                     // read's last real op, if here
+            const bool has_last = lane_live && lr >= 0 && lr < OPL && (uint32_t)lr < nb;   // reached, no break
+            if (COUNT) live_ops += lane_live ? (uint32_t)min((int32_t)nb + 1, nreal) : 0u;
+            const uint32_t pushm = candm & livem;
+            const bool stop = KIND != K_INS && (brk || has_last);
+            if (pushm || stop) {
+                // rare: candidates (A4-A6) and the soft-clip candidate of the read's stop op
+                const int32_t si = brk ? (int32_t)nb : lr;                 // stop op index
+                uint32_t stop_after = 0;
+#pragma unroll
+                for (int i = 0; i < OPL; i++) {
+                    const uint32_t before = pre + (i ? Pi[i - 1] : 0u), after = pre + Pi[i];
+                    if ((pushm >> i) & 1u) {
+                        const uint32_t len = wv[i] >> 4;
+                        sink.push1(KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before);   // :198 / :136
+                    }
+                    if (i == si) stop_after = after;
                 }
-                if (KIND != K_INS) {
-                    const bool is_last = vi && (jb + i + 1 == blk_end || ((lastm >> i) & 1u));
-                    if (brk || (lvop && is_last)) {           // this read's walk stops here
-                        const uint32_t kc = L.clip[k];
-                        if (KIND == K_START) {                // trailing S, no break, s <= rp <= e (:152)
-                            if (!brk && (kc & SVT_CLIP_LAST_S) && s <= after && after <= e) sink.push1((int32_t)after);
-                            if (COUNT && brk && !is_last) live_ops++;   // cigar[n-1] test word
-                        } else {                              // leading S and s <= pos <= e: rp + 1 (:210-220)
-                            const uint32_t kp = L.rpos[k];
-                            if ((kc & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)kp && (int64_t)kp <= (int64_t)e)
-                                sink.push1((int32_t)(after + 1u));
-                        }
+                if (KIND != K_INS && stop) {
+                    const uint2 mt = L.meta[kl];
+                    if (KIND == K_START) {   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
+                        if (!brk && (mt.y & SVT_CLIP_LAST_S) && s <= stop_after) sink.push1((int32_t)stop_after);
+                        if (COUNT && brk && (int32_t)nb != lr) live_ops++;        // cigar[n-1] test word
+                    } else {                 // leading S and s <= pos <= e: walked rp + 1  (:210-220)
+                        if ((mt.y & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)mt.x && (int64_t)mt.x <= (int64_t)e)
+                            sink.push1((int32_t)(stop_after + 1u));
                     }
                 }
             }
             carry_rp = next_carry_rp;
             carry_k = next_carry_k;
             J = Jn;
-            A = An;
         }
         // reads whose walk could wrap uint32: exact per-read replay
         uint64_t sm = ballot(ovl && slow);
@@ -873,13 +861,13 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
 
     std::vector<int32_t> emax((size_t)nr), maxspan((size_t)(nt > 0 ? nt : 1), 0);
     std::vector<uint4> rec((size_t)nr);
+    std::vector<uint64_t> poff((size_t)nr + 1, 0);   // padded CIGAR offsets (multiples of OPL)
     std::vector<int64_t> bkt_off((size_t)nt + 1, 0);
     std::vector<uint32_t> bkt;
+    uint64_t pw = 0;
     for (int32_t t = 0; t < nt; t++) {
         const int64_t r0 = p->tid_off[t], r1 = p->tid_off[t + 1];
         if (r1 - r0 > 0xffffffffll) return fail(c, SVT_EINVAL, "pileup: %s", "> 2^32 reads on one contig");
-        if (r1 > r0 && p->cig_off[r1] - p->cig_off[r0] >= (1ull << 31))
-            return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^31 CIGAR ops on one contig");
         int32_t m = INT32_MIN, ms = 0, maxpos = 0;
         for (int64_t r = r0; r < r1; r++) {
             if (r > r0 && p->pos[r] < p->pos[r - 1])
@@ -905,9 +893,13 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
             if (p->endpos[r] - p->pos[r] > ms) ms = p->endpos[r] - p->pos[r];
             maxpos = std::max(maxpos, p->pos[r]);
             emax[(size_t)r] = m;
+            poff[(size_t)r] = pw;
             rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | slow | (clip << 30),
-                                        (uint32_t)o0);
+                                        (uint32_t)pw);
+            pw += ((uint64_t)ncig + (OPL - 1)) & ~(uint64_t)(OPL - 1);
         }
+        if (r1 > r0 && pw - poff[(size_t)r0] >= (1ull << 31))
+            return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^31 CIGAR ops on one contig");
         maxspan[(size_t)t] = ms;
         // bucket b: first contig-relative read with pos >= b << BKT_SHIFT, b = 0..nb-1
         const int64_t nb = (r1 > r0 ? ((int64_t)maxpos >> BKT_SHIFT) + 2 : 1) + 1;
@@ -918,18 +910,25 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
             bkt.push_back((uint32_t)(r - r0));
         }
     }
+    poff[(size_t)nr] = pw;
     bkt_off[(size_t)nt] = (int64_t)bkt.size();
+    // padded arena: read r's ops at poff[r], zero words (0M) up to the next multiple of OPL
+    std::vector<uint32_t> arena((size_t)pw + CIGAR_PAD, 0u);
+    for (int64_t r = 0; r < nr; r++) {
+        uint64_t o0 = p->cig_off[r], n = p->cig_off[r + 1] - o0;
+        if (n) memcpy(arena.data() + poff[(size_t)r], p->cigar + o0, n * 4);
+    }
     svt_status s;
     if ((s = upload(c, c->d_pos, p->pos, (size_t)nr))) return s;
     if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
     if ((s = upload(c, c->d_rec, rec.data(), (size_t)nr))) return s;
-    if ((s = upload(c, c->d_off64, p->cig_off, nr > 0 ? (size_t)nr + 1 : 0, nr > 0 ? 0 : 1))) return s;
+    if ((s = upload(c, c->d_off64, poff.data(), poff.size()))) return s;
     if ((s = upload(c, c->d_maxspan, maxspan.data(), maxspan.size()))) return s;
     if ((s = upload(c, c->d_bkt, bkt.data(), bkt.size()))) return s;
     if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
     if (nt > 0) { if ((s = upload(c, c->d_tid_off, p->tid_off, (size_t)nt + 1))) return s; }
     else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
-    if ((s = upload(c, c->d_cigar, p->cigar, (size_t)nops, CIGAR_PAD))) return s;
+    if ((s = upload(c, c->d_cigar, arena.data(), arena.size()))) return s;
     c->n_targets = nt;
     c->n_reads = nr;
     c->n_ops = nops;
