@@ -90,6 +90,14 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ int32_t uniform_i(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// Every window is owned by ONE wave (several independent waves share a workgroup), so the
+// only ordering ever needed is between the lanes of a wave: a workgroup-scope
+// release/acquire pair around a wave barrier (no s_barrier across the workgroup).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -336,7 +344,7 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
         const bool live = ovl && !slow && ncig > 0;
         const int nblk = (int)min<int64_t>(WAVE, hi - rb);
         const int32_t blk_end = rdlane_i(en_pad, nblk - 1);
-        __syncthreads();
+        wave_sync();
         L.walk[ln] = make_uint2(live ? rpos : dead_rp, (uint32_t)(st0 + (int32_t)ncig));
         L.meta[ln] = make_uint2(rpos, clip);
 
@@ -371,9 +379,9 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
             // ---- which lanes start a read
             L.slot[ln] = -1;
             if (ln == 0) L.slot[WAVE] = -1;
-            __syncthreads();
+            wave_sync();
             if (ncig > 0 && inb && st0 >= A && st0 <= A + TILE) L.slot[(st0 - A) / OPL] = (int8_t)ln;
-            __syncthreads();
+            wave_sync();
             const int32_t hk = lane_ok ? (int32_t)L.slot[ln] : -1;
             const int32_t kinc = wave_scan_max(hk);
             const int32_t kl = max(carry_k, kinc);           // this lane's read
@@ -490,7 +498,7 @@ __device__ __forceinline__ void wave_bitonic_sort(int32_t *buf, int N) {
                     if ((a > b) == up) { buf[i] = b; buf[p] = a; }
                 }
             }
-            __syncthreads();
+            wave_sync();
         }
     }
 }
@@ -590,7 +598,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
     int N = 1;
     while (N < n) N <<= 1;
     for (int i = n + ln; i < N; i += WAVE) buf[i] = INT32_MAX;
-    __syncthreads();
+    wave_sync();
     wave_bitonic_sort(buf, N);
     int64_t carry = 0;
     if (ln == 0) P[0] = 0;
@@ -601,7 +609,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
         if (i < n) P[i + 1] = s;
         carry = (int64_t)rdlane64((uint64_t)s, WAVE - 1);
     }
-    __syncthreads();
+    wave_sync();
     return vote(buf, P, n, pos, k);
 }
 
@@ -618,10 +626,10 @@ template <int KIND, bool COUNT, bool STREAM>
 __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
                                           StreamLds &L) {
     if (lane_id() == 0) *sink.cnt = 0;
-    __syncthreads();
+    wave_sync();
     if (STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L);
     else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
-    __syncthreads();
+    wave_sync();
     return uniform_i(*sink.cnt);
 }
 
@@ -656,13 +664,20 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     return sort_and_vote(g, gp, n, (int32_t)imprecise, a.prm);
 }
 
-// grid = 2 * n_loci workgroups of one wave: workgroup 2i refines locus i's first window
-// (DEL: refine_start, INS: refine_ins), 2i+1 its second (DEL: refine_end).
+// One wave per query window, WPB independent waves per workgroup.  Window g < n is locus
+// g's first window (DEL: refine_start over [pos-wider, pos+narrow], INS: refine_ins),
+// window n + i is locus i's second (DEL: refine_end over end +- narrow): the wide windows
+// are dispatched first, so the short ones fill the tail.
+constexpr int WPB = 4;
+
 template <bool COUNT, bool STREAM>
-__global__ __launch_bounds__(64) void refine_kernel(KArgs a) {
-    __shared__ WinLds lds;
-    const uint32_t li = blockIdx.x >> 1, w = blockIdx.x & 1;
-    if (li >= a.n) return;
+__global__ __launch_bounds__(64 * WPB) void refine_kernel(KArgs a) {
+    __shared__ WinLds lds_all[WPB];
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x * WPB + wid;
+    if (g >= 2 * a.n) return;
+    WinLds &lds = lds_all[wid];
+    const uint32_t w = g >= a.n ? 1u : 0u, li = g - w * a.n;
     const svt_locus L = a.loci[li];
     const int32_t type = uniform_i(L.type), chrom = uniform_i(L.chrom);
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
@@ -771,7 +786,7 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     if (n > 0x3fffffffull) return fail(c, SVT_EINVAL, "batch too large (%s)", "n > 2^30-1");
     HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 64, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
-    dim3 grid((unsigned)(2 * n)), block(64);
+    dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
     if (c->stream_gather) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, true>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((refine_kernel<false, true>), grid, block, 0, st, a);
