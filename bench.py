@@ -48,24 +48,29 @@ def cpu_baseline(res, n_threads: int, budget_s: float = 20.0) -> dict:
     import oracle_ffi as O  # noqa: E402
 
     loci = res.loci
-    # calibrate on a small prefix, then size the sample to ~budget_s of CPU work
+
+    def timed(n: int, threads: int, min_s: float) -> tuple[float, int]:
+        """loci/s over repeated passes on loci[:n] until at least min_s of wall time."""
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.refine_batch(res.pileup, loci[:n], threads=threads)
+            done += n
+            dt = time.perf_counter() - t0
+            if dt >= min_s:
+                return done / dt, done
+
     n0 = min(len(loci), 500)
     t = time.perf_counter()
     O.refine_batch(res.pileup, loci[:n0], threads=1)
-    dt = max(time.perf_counter() - t, 1e-6)
-    per_locus_1t = dt / n0
+    per_locus_1t = max(time.perf_counter() - t, 1e-6) / n0
     n1 = int(min(len(loci), max(n0, budget_s / 3 / per_locus_1t)))
-    t = time.perf_counter()
-    O.refine_batch(res.pileup, loci[:n1], threads=1)
-    v1 = n1 / (time.perf_counter() - t)
-    nt = int(min(len(loci), max(n0, budget_s * 2 / 3 / per_locus_1t * n_threads / 2)))
-    t = time.perf_counter()
-    O.refine_batch(res.pileup, loci[:nt], threads=n_threads)
-    vt = nt / (time.perf_counter() - t)
+    v1, d1 = timed(n1, 1, budget_s / 3)
+    vt, dt_ = timed(len(loci), n_threads, budget_s * 2 / 3)
     return {
         "value": round(vt, 1), "unit": "loci/s", "cores": n_threads, "kind": "port",
-        "sample": f"first {nt} loci of the same workload, in-memory columnar pileup (no BGZF inflate), "
-                  f"{n_threads} pthread workers on {_cpu_model()}; 1 thread: {v1:.1f} loci/s on {n1} loci",
+        "sample": f"all {len(loci)} loci of the same workload, repeated for >= {budget_s * 2 / 3:.0f} s "
+                  f"({dt_} loci), in-memory columnar pileup (no BGZF inflate), {n_threads} pthread workers on "
+                  f"{_cpu_model()}; 1 thread: {v1:.1f} loci/s over {d1} loci (first {n1})",
         "value_1thread": round(v1, 1),
     }
 
@@ -161,6 +166,18 @@ def main() -> int:
     alg_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
     achieved = alg_bytes / (kern_mean_ms * 1e-3) / 1e9
 
+    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes, when they
+    # were taken on this engine version and workload (tools/gpu_profile.sh -> profiles/traffic.json)
+    traffic = traffic_src = None
+    try:
+        from svtrek_amd import version as _ver
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            tj = json.load(f)
+        if tj.get("engine_version") == _ver() and tj.get("workload") == args.workload:
+            traffic, traffic_src = int(tj["hbm_bytes_per_launch"]), tj.get("source")
+    except (OSError, ValueError, KeyError):
+        pass
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -189,7 +206,9 @@ def main() -> int:
                        "read_len_mean": cfg.read_len_mean, "parallelism": f"loci-shard x{world}",
                        "gather": bool(world > 1 and not args.no_gather)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_gbs": round(traffic / (kern_mean_ms * 1e-3) / 1e9, 2) if traffic else None,
+                         "traffic_source": traffic_src,
                          "kernel": "refine_kernel", "kernel_ms_mean": round(kern_mean_ms, 5),
                          "kernel_ms_min": round(kern_ms[0], 5), "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
