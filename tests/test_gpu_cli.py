@@ -88,3 +88,18 @@ def test_cli_usage_and_missing_files(tmp_path):
     assert r.returncode == 0 and "--consensus-min-count" in r.stdout
     r = run_cli("-v", str(tmp_path / "none.vcf"), check=False)
     assert r.returncode != 0 and "[ERROR] BAM file is not provided." in r.stderr
+
+
+def test_audt_dist_single_rank(tmp_path):
+    """The torchrun multi-GPU driver (svtrek_amd.audt_dist) at world size 1 prints the same bytes."""
+    import sys
+    r = sim.generate(sim.SimConfig(seed=51, n_targets=2, n_loci=150, del_frac=0.5, coverage=15), keep_handle=True)
+    bam = str(tmp_path / "d.bam")
+    sim.write_bam(r, bam)
+    vcf = tmp_path / "d.vcf"
+    sim.write_vcf(r.loci, str(vcf))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    res = subprocess.run([sys.executable, "-m", "svtrek_amd.audt_dist", "-b", bam, "-v", str(vcf)],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600, cwd=ROOT, env=env)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert res.stdout == O.audit_text(vcf.read_text(), r.pileup)
