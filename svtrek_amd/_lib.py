@@ -72,7 +72,8 @@ _engine = None
 
 
 def engine_path() -> str:
-    return os.path.join(PKG, "libsvtrek_hip.so")
+    """The in-tree engine; SVTREK_ENGINE_LIB may name a variant build (A/B benchmarking)."""
+    return os.environ.get("SVTREK_ENGINE_LIB") or os.path.join(PKG, "libsvtrek_hip.so")
 
 
 def load_engine() -> C.CDLL:

@@ -306,8 +306,11 @@ __device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint
 // HBM layout (svt_load_pileup): every read's CIGAR starts on a multiple of OPL words and
 // is padded with zero words (0M: advances nothing, never a candidate) to the next
 // multiple, so each lane's OPL ops of a tile belong to exactly one read.
-constexpr int OPL = 8;                      // CIGAR ops per lane per tile
-constexpr int TILE = OPL * WAVE;            // 512 ops (2 KiB) per stream step
+#ifndef SVT_OPL
+#define SVT_OPL 8
+#endif
+constexpr int OPL = SVT_OPL;                // CIGAR ops per lane per tile (4, 8 or 16)
+constexpr int TILE = OPL * WAVE;            // 512 ops (2 KiB) per stream step at OPL 8
 
 struct StreamLds {
     int8_t slot[WAVE + 4];   // per tile lane slot: block-relative index of the read starting there, else -1
