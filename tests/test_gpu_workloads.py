@@ -1,0 +1,45 @@
+"""BASELINE.json configs 3-5 read models at parity-test sizes: every locus bit-exact vs the
+oracle, and the device work counters equal the oracle's (the roofline's algorithmic bytes)."""
+from dataclasses import replace
+
+import numpy as np
+import oracle_ffi as O
+import pytest
+
+from svtrek_amd import sim
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(engine_factory, cfg, threads=8):
+    r = sim.generate(cfg)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    got = eng.refine(r.loci)
+    want, ow = O.refine_batch(r.pileup, r.loci, threads=threads, with_work=True)
+    bad = np.nonzero((got["start"] != want["start"]) | (got["end"] != want["end"]))[0]
+    assert len(bad) == 0, f"{len(bad)} loci differ, first {r.loci[bad[0]]}: gpu {got[bad[0]]} oracle {want[bad[0]]}"
+    w = eng.count_work(r.loci)
+    assert (w["reads"], w["ops_walked"], w["candidates"]) == (ow["reads"], ow["ops_walked"], ow["candidates"])
+    return r, got
+
+
+def test_cfg3_del_ins_mix_subset(engine_factory):
+    cfg = replace(sim.WORKLOADS["cfg3_50k_delins_30x_ont"], n_loci=3000, n_targets=2)
+    r, got = _check(engine_factory, cfg)
+    ins = r.loci["type"] == 1
+    assert ins.any() and (~ins).any()
+    assert (got["start"][ins] != 0xFFFFFFFF).mean() > 0.5          # INS refined
+    assert (got["end"][ins] == 0xFFFFFFFF).all()                   # INS has no end window
+
+
+def test_cfg4_hifi_dense_subset(engine_factory):
+    """HiFi-like (15 kb, ~30 ops/read) with loci every ~3 kb: windows overlap heavily."""
+    cfg = replace(sim.WORKLOADS["cfg4_1m_delins_30x_hifi"], n_loci=20000, n_targets=2)
+    _check(engine_factory, cfg)
+
+
+def test_cfg5_ultralong_subset(engine_factory):
+    """60x ultra-long (50 kb, ~2000 ops/read): deep pileups, reads crossing several tiles."""
+    cfg = replace(sim.WORKLOADS["cfg5_100k_60x_ul_ont"], n_loci=400, n_targets=1)
+    _check(engine_factory, cfg)
