@@ -672,6 +672,9 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
 // window n + i is locus i's second (DEL: refine_end over end +- narrow): the wide windows
 // are dispatched first, so the short ones fill the tail.
 constexpr int WPB = 4;
+#ifndef SVT_INTERLEAVE_WINDOWS
+#define SVT_INTERLEAVE_WINDOWS 0
+#endif
 
 template <bool COUNT, bool STREAM>
 __global__ __launch_bounds__(64 * WPB) void refine_kernel(KArgs a) {
@@ -680,7 +683,11 @@ __global__ __launch_bounds__(64 * WPB) void refine_kernel(KArgs a) {
     const uint32_t g = blockIdx.x * WPB + wid;
     if (g >= 2 * a.n) return;
     WinLds &lds = lds_all[wid];
+#if SVT_INTERLEAVE_WINDOWS
+    const uint32_t w = g & 1u, li = g >> 1;      // a locus' two windows back to back (L2/MALL reuse)
+#else
     const uint32_t w = g >= a.n ? 1u : 0u, li = g - w * a.n;
+#endif
     const svt_locus L = a.loci[li];
     const int32_t type = uniform_i(L.type), chrom = uniform_i(L.chrom);
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
