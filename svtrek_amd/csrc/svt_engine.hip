@@ -309,6 +309,12 @@ __device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint
 #ifndef SVT_OPL
 #define SVT_OPL 8
 #endif
+#ifndef SVT_JUMP
+#define SVT_JUMP 1               // skip the rest of a read that broke / yields nothing
+#endif
+#ifndef SVT_EARLY_PREFETCH
+#define SVT_EARLY_PREFETCH 0     // prefetch the contiguous next tile before working on this one
+#endif
 constexpr int OPL = SVT_OPL;                // CIGAR ops per lane per tile (4, 8 or 16)
 constexpr int TILE = OPL * WAVE;            // 512 ops (2 KiB) per stream step at OPL 8
 
@@ -396,12 +402,22 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
             for (int q = 0; q < OPL / 4; q++) {
                 wv[4 * q] = cw[q].x; wv[4 * q + 1] = cw[q].y; wv[4 * q + 2] = cw[q].z; wv[4 * q + 3] = cw[q].w;
             }
+#if SVT_EARLY_PREFETCH
+            // speculative prefetch of the contiguous next tile, issued before any work on this
+            // one; re-issued below only when the read at U turns out to be finished
+            if (U < blk_end) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)U + OPL * ln);
+#pragma unroll
+                for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
+            }
+#endif
             uint32_t Pi[OPL], T = 0, candm = 0;
 #pragma unroll
             for (int i = 0; i < OPL; i++) {
                 const uint32_t op = wv[i] & 0xfu, len = wv[i] >> 4;
-                const uint32_t keep = ((0x12u >> op) & 1u) ^ 1u;   // op not in {I, S}: refinement.c:141
-                T += len & (0u - keep);
+                // bit `op` of ~0x12 (bits I=1, S=4 clear), sign-extended: all ones iff op advances rp
+                const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)~0x12u, op, 1);   // refinement.c:141
+                T += len & keep;
                 Pi[i] = T;
                 candm |= (uint32_t)is_candidate_op<KIND>(op, len) << i;
             }
@@ -419,7 +435,7 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
             // ---- next tile: continue the read at U unless it already broke / yields nothing;
             //      otherwise jump to the next read that yields.  Prefetch it now.
             int32_t Jn = U;
-            {
+            if (SVT_JUMP) {
                 const int32_t kc = next_carry_k;
                 const bool cont = kc >= 0 && U < rdlane_i(en_pad, kc);
                 if (!(cont && next_carry_rp <= e)) {
@@ -427,7 +443,7 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
                     Jn = later ? max(U, rdlane_i(st0, __builtin_ctzll(later))) : blk_end;
                 }
             }
-            if (Jn < blk_end) {   // cw is dead once wv is unpacked: reuse it for the prefetch
+            if (Jn < blk_end && (!SVT_EARLY_PREFETCH || Jn != U)) {   // cw is dead once wv is unpacked
                 const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)Jn + OPL * ln);
 #pragma unroll
                 for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
