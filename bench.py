@@ -84,6 +84,8 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--replicate", type=int, default=1,
+                    help="diagnostic: launch the workload's loci R times per step (tail-effect study)")
     args = ap.parse_args()
 
     import torch
@@ -118,6 +120,11 @@ def main() -> int:
     load_s = time.perf_counter() - t0
     work = eng.count_work(res.loci)   # exact algorithmic work (diagnostic launch, untimed)
 
+    if args.replicate > 1:
+        import numpy as np
+        res.loci = np.tile(res.loci, args.replicate)
+        n = len(res.loci)
+        work = {k: v * args.replicate for k, v in work.items()}
     loci_np = res.loci.view("u1").reshape(-1)
     d_loci = torch.from_numpy(loci_np.copy()).to(dev)
     d_out = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
