@@ -280,10 +280,23 @@ __device__ __forceinline__ bool read_range(const DevPileup &P, int tid, int64_t 
 
 // The yielded reads of a window are split evenly over the waves of its workgroup: part p
 // of n takes reads [lo + m*p/n, lo + m*(p+1)/n), m = hi - lo (candidates are a multiset).
-__device__ __forceinline__ bool split_range(int64_t &lo, int64_t &hi, int part, int nparts) {
-    const int64_t m = hi - lo, l0 = lo;
-    lo = l0 + m * part / nparts;
-    hi = l0 + m * (part + 1) / nparts;
+#ifndef SVT_SPLIT_BY_OPS
+#define SVT_SPLIT_BY_OPS 0
+#endif
+__device__ __forceinline__ bool split_range(int64_t &lo, int64_t &hi, int part, int nparts, const uint64_t *off64) {
+    const int64_t m = hi - lo, l0 = lo, h0 = hi;
+    if (!SVT_SPLIT_BY_OPS || nparts == 1 || m <= nparts) {
+        lo = l0 + m * part / nparts;
+        hi = l0 + m * (part + 1) / nparts;
+        return lo < hi;
+    }
+    // equal shares of the window's CIGAR span: part p starts at the first read whose
+    // padded offset reaches S0 + span*p/n
+    const uint64_t a0 = off64[l0], span = off64[h0] - a0;
+    const uint64_t t0 = a0 + span * (uint64_t)part / (uint64_t)nparts;
+    const uint64_t t1 = a0 + span * (uint64_t)(part + 1) / (uint64_t)nparts;
+    lo = part == 0 ? l0 : wave_partition_point(l0, h0, [&](int64_t r) { return off64[r] >= t0; });
+    hi = part == nparts - 1 ? h0 : wave_partition_point(l0, h0, [&](int64_t r) { return off64[r] >= t1; });
     return lo < hi;
 }
 
@@ -293,7 +306,7 @@ __device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint
                                                int part, int nparts) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi) || !split_range(lo, hi, part, nparts)) return;
+    if (!read_range(P, tid, beg, end, lo, hi) || !split_range(lo, hi, part, nparts, P.off64)) return;
     const int ln = lane_id();
     for (int64_t base = lo; base < hi; base += WAVE) {
         int64_t r = base + ln;
@@ -341,7 +354,7 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
     if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st, part, nparts); return; }
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi) || !split_range(lo, hi, part, nparts)) return;
+    if (!read_range(P, tid, beg, end, lo, hi) || !split_range(lo, hi, part, nparts, P.off64)) return;
     const int ln = lane_id();
     const uint64_t S0 = P.off64[lo];
     const uint32_t base32 = (uint32_t)S0;
