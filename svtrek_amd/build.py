@@ -52,7 +52,7 @@ def build_host(force: bool = False) -> str:
     hdrs = [os.path.join(CSRC, "svtrek_host.h"), os.path.join(INC, "svtrek_gpu.h")]
     if all(os.path.exists(s) for s in srcs) and (force or _stale(out, srcs + hdrs)):
         _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-pthread",
-              "-I", INC, "-o", out] + srcs + ["-lz"])
+              "-I", INC, "-o", out] + srcs + ["-lz", "-ldl"])
     return out
 
 
@@ -64,7 +64,7 @@ def build_cli(force: bool = False) -> str:
     eng = os.path.join(PKG, "libsvtrek_hip.so")
     if all(os.path.exists(s) for s in srcs) and (force or _stale(out, srcs + hdrs + [eng])):
         _run(["g++", "-O3", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-I", INC, "-o", out] + srcs +
-             ["-L", PKG, "-lsvtrek_hip", "-Wl,-rpath,$ORIGIN", "-lz"])
+             ["-L", PKG, "-lsvtrek_hip", "-Wl,-rpath,$ORIGIN", "-lz", "-ldl"])
     return out
 
 

@@ -6,12 +6,21 @@
 // CIGAR from its CG:B,I tag (htslib bam_tag2cigar) -- plus the two words the soft-clip
 // tests read (cigar[n_cigar-1] and cigar[0], which for n_cigar == 0 land in the padded
 // read name / the SEQ bytes of htslib's bam1_t data layout).  This reader extracts
-// exactly those, once per file: BGZF blocks are inflated in parallel in bounded chunks,
-// records are parsed sequentially, and SEQ/QUAL/aux are dropped.
+// exactly those, once per file, in bounded chunks:
+//   1. parallel raw-inflate of the chunk's BGZF blocks (libdeflate if present, else zlib;
+//      T threads);
+//   2. a sequential scan of the record boundaries (4 bytes per record);
+//   3. parallel per-record extraction in two passes (CIGAR lengths incl. CG tags, then
+//      copies into the final arrays at prefix-summed offsets).
+// A coordinate-sorted BAM (the only kind that has a BAI) needs no reordering; other
+// files are stably sorted by (tid, pos) at the end.  SEQ/QUAL/aux are never copied.
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -27,6 +36,40 @@ constexpr uint32_t OP_M = 0, OP_D = 2, OP_N = 3, OP_S = 4, OP_EQ = 7, OP_X = 8;
 inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
 
+template <typename F>
+void parallel_for(int threads, size_t n, F &&f) {   // f(begin, end) over contiguous slices
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), n / 4096 + 1));
+    if (T == 1) { f((size_t)0, n); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
+    for (auto &x : th) x.join();
+}
+
+// Raw-DEFLATE block decoder: libdeflate when the system has it (libdeflate.so.0, bound at
+// run time through its stable C API: alloc / deflate_decompress / free), zlib otherwise.
+struct Inflater {
+    using alloc_t = void *(*)();
+    using dec_t = int (*)(void *, const void *, size_t, void *, size_t, size_t *);
+    using free_t = void (*)(void *);
+    alloc_t ld_alloc = nullptr;
+    dec_t ld_dec = nullptr;
+    free_t ld_free = nullptr;
+    Inflater() {
+        if (getenv("SVTREK_NO_LIBDEFLATE")) return;
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        ld_alloc = (alloc_t)dlsym(h, "libdeflate_alloc_decompressor");
+        ld_dec = (dec_t)dlsym(h, "libdeflate_deflate_decompress");
+        ld_free = (free_t)dlsym(h, "libdeflate_free_decompressor");
+        if (!ld_alloc || !ld_dec || !ld_free) ld_alloc = nullptr;
+    }
+    bool fast() const { return ld_alloc != nullptr; }
+};
+const Inflater &inflater() {
+    static const Inflater inf;
+    return inf;
+}
+
 struct BgzfReader {
     FILE *f = nullptr;
     int threads = 1;
@@ -37,90 +80,80 @@ struct BgzfReader {
     // Append the next batch of inflated blocks to `out`; false at end of file / on error.
     bool next(std::vector<uint8_t> &out) {
         const size_t CHUNK = 64u << 20;
-        if (!eof) {
-            size_t old = comp.size();
-            comp.resize(old + CHUNK);
-            size_t got = fread(comp.data() + old, 1, CHUNK, f);
-            comp.resize(old + got);
-            if (got < CHUNK) eof = true;
-        }
-        // index complete blocks
-        struct Blk { size_t off, clen, ulen, cdata; };
-        std::vector<Blk> blks;
-        size_t p = 0;
-        while (p + 18 <= comp.size()) {
-            const uint8_t *h = comp.data() + p;
-            if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { err = "not a BGZF file (bad gzip header)"; return false; }
-            uint16_t xlen = rd16(h + 10);
-            if (p + 12 + xlen > comp.size()) break;
-            size_t bsize = 0;
-            for (size_t x = 0; x + 4 <= xlen;) {
-                const uint8_t *sf = h + 12 + x;
-                uint16_t slen = rd16(sf + 2);
-                if (sf[0] == 66 && sf[1] == 67 && slen == 2) bsize = (size_t)rd16(sf + 4) + 1;
-                x += 4 + slen;
+        for (;;) {
+            if (!eof) {
+                size_t old = comp.size();
+                comp.resize(old + CHUNK);
+                size_t got = fread(comp.data() + old, 1, CHUNK, f);
+                comp.resize(old + got);
+                if (got < CHUNK) eof = true;
             }
-            if (!bsize) { err = "BGZF block without BC subfield"; return false; }
-            if (p + bsize > comp.size()) break;
-            size_t cdata = p + 12 + xlen, clen = bsize - xlen - 20;
-            uint32_t isize = rd32(comp.data() + p + bsize - 4);
-            blks.push_back({p, clen, isize, cdata});
-            p += bsize;
-        }
-        if (blks.empty()) {
-            if (eof && !comp.empty()) { err = "truncated BGZF block at end of file"; return false; }
-            return !(eof && comp.empty()) && !comp.empty() ? false : false;
-        }
-        std::vector<size_t> uoff(blks.size() + 1, 0);
-        for (size_t i = 0; i < blks.size(); i++) uoff[i + 1] = uoff[i] + blks[i].ulen;
-        size_t base = out.size();
-        out.resize(base + uoff.back());
-        std::vector<int> bad(blks.size(), 0);
-        auto work = [&](int t) {
-            z_stream zs;
-            memset(&zs, 0, sizeof zs);
-            if (inflateInit2(&zs, -15) != Z_OK) { bad[0] = 1; return; }
-            for (size_t i = (size_t)t; i < blks.size(); i += (size_t)threads) {
-                inflateReset(&zs);
-                zs.next_in = comp.data() + blks[i].cdata;
-                zs.avail_in = (uInt)blks[i].clen;
-                zs.next_out = out.data() + base + uoff[i];
-                zs.avail_out = (uInt)blks[i].ulen;
-                int rc = inflate(&zs, Z_FINISH);
-                if (rc != Z_STREAM_END || zs.total_out != blks[i].ulen) bad[i] = 1;
-                zs.total_out = 0;
+            struct Blk { size_t clen, ulen, cdata; };
+            std::vector<Blk> blks;
+            size_t p = 0;
+            while (p + 18 <= comp.size()) {
+                const uint8_t *h = comp.data() + p;
+                if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { err = "not a BGZF file (bad gzip header)"; return false; }
+                uint16_t xlen = rd16(h + 10);
+                if (p + 12 + xlen > comp.size()) break;
+                size_t bsize = 0;
+                for (size_t x = 0; x + 4 <= xlen;) {
+                    const uint8_t *sf = h + 12 + x;
+                    uint16_t slen = rd16(sf + 2);
+                    if (sf[0] == 66 && sf[1] == 67 && slen == 2) bsize = (size_t)rd16(sf + 4) + 1;
+                    x += 4 + slen;
+                }
+                if (!bsize) { err = "BGZF block without BC subfield"; return false; }
+                if (p + bsize > comp.size()) break;
+                blks.push_back({bsize - xlen - 20, rd32(comp.data() + p + bsize - 4), p + 12 + xlen});
+                p += bsize;
             }
-            inflateEnd(&zs);
-        };
-        int nt = std::max(1, std::min<int>(threads, (int)blks.size()));
-        if (nt == 1) work(0);
-        else {
-            std::vector<std::thread> th;
-            for (int t = 0; t < nt; t++) th.emplace_back(work, t);
-            for (auto &x : th) x.join();
+            if (blks.empty()) {
+                if (eof) {
+                    if (!comp.empty()) err = "truncated BGZF block at end of file";
+                    return false;
+                }
+                continue;   // a single block larger than what was read so far
+            }
+            std::vector<size_t> uoff(blks.size() + 1, 0);
+            for (size_t i = 0; i < blks.size(); i++) uoff[i + 1] = uoff[i] + blks[i].ulen;
+            const size_t base = out.size();
+            out.resize(base + uoff.back());
+            std::atomic<int> bad{0};
+            const Inflater &inf = inflater();
+            parallel_for(threads, blks.size() * 4096, [&](size_t b0, size_t b1) {
+                if (inf.fast()) {
+                    void *d = inf.ld_alloc();
+                    if (!d) { bad = 1; return; }
+                    for (size_t i = b0 / 4096; i < b1 / 4096; i++) {
+                        size_t got = 0;
+                        int rc = inf.ld_dec(d, comp.data() + blks[i].cdata, blks[i].clen, out.data() + base + uoff[i],
+                                            blks[i].ulen, &got);
+                        if (rc != 0 || got != blks[i].ulen) bad = 1;
+                    }
+                    inf.ld_free(d);
+                    return;
+                }
+                z_stream zs;
+                memset(&zs, 0, sizeof zs);
+                if (inflateInit2(&zs, -15) != Z_OK) { bad = 1; return; }
+                for (size_t i = b0 / 4096; i < b1 / 4096; i++) {
+                    inflateReset(&zs);
+                    zs.next_in = comp.data() + blks[i].cdata;
+                    zs.avail_in = (uInt)blks[i].clen;
+                    zs.next_out = out.data() + base + uoff[i];
+                    zs.avail_out = (uInt)blks[i].ulen;
+                    int rc = inflate(&zs, Z_FINISH);
+                    if (rc != Z_STREAM_END || zs.total_out != blks[i].ulen) bad = 1;
+                }
+                inflateEnd(&zs);
+            });
+            if (bad) { err = "corrupt BGZF block (inflate failed)"; return false; }
+            comp.erase(comp.begin(), comp.begin() + (ptrdiff_t)p);
+            return true;
         }
-        for (size_t i = 0; i < blks.size(); i++)
-            if (bad[i]) { err = "corrupt BGZF block (inflate failed)"; return false; }
-        comp.erase(comp.begin(), comp.begin() + (ptrdiff_t)p);
-        return true;
     }
 };
-
-}  // namespace
-
-struct svth_bam {
-    std::vector<std::string> names;
-    std::vector<int64_t> tid_off;
-    std::vector<int32_t> pos, endpos;
-    std::vector<uint64_t> cig_off;
-    std::vector<uint32_t> cigar;
-    std::vector<uint8_t> clip;
-    int64_t n_records = 0, n_cg = 0;
-};
-
-namespace {
-
-struct RawRead { int32_t tid, pos, endpos; uint64_t off; uint32_t n; uint8_t clip; int64_t seq; };
 
 // htslib bam_tag2cigar's conditions: n_cigar > 0, tid >= 0, pos >= 0, cigar[0] == <l_seq>S,
 // a CG tag of type B,I (or B,i) with at least n_cigar elements and fewer than 2^29.
@@ -166,7 +199,101 @@ bool find_cg(const uint8_t *aux, const uint8_t *end, const uint8_t **arr, uint32
     return false;
 }
 
+// Where one record's CIGAR lives (after CG restoration) and its soft-clip test bits.
+struct RecView {
+    const uint8_t *cig;
+    uint32_t n;
+    bool cg;
+    bool ok;
+    int32_t tid, pos;
+    uint16_t flag;
+    uint8_t clip;
+};
+
+RecView view_record(const uint8_t *r, uint32_t bs, int32_t n_ref) {
+    RecView v{};
+    const uint8_t *rend = r + bs;
+    v.tid = (int32_t)rd32(r);
+    v.pos = (int32_t)rd32(r + 4);
+    const uint32_t l_qname = r[8];
+    const uint16_t n_cig = rd16(r + 12);
+    v.flag = rd16(r + 14);
+    const int32_t l_seq = (int32_t)rd32(r + 16);
+    v.ok = v.tid >= 0 && v.tid < n_ref && v.pos >= 0;   // only these can be yielded by a tid >= 0 query
+    if (!v.ok) return v;
+    const uint8_t *qn = r + 32, *cg = qn + l_qname;
+    if (cg + 4ull * n_cig > rend || l_seq < 0) { v.ok = false; v.n = 0xffffffffu; return v; }
+    const uint8_t *after = cg + 4ull * n_cig;   // SEQ starts here
+    const uint8_t *aux = after + (size_t)(l_seq + 1) / 2 + (size_t)l_seq;
+    v.cig = cg;
+    v.n = n_cig;
+    if (n_cig > 0 && (rd32(cg) & 0xfu) == OP_S && (int64_t)(rd32(cg) >> 4) == l_seq && aux <= rend) {
+        const uint8_t *arr;
+        uint32_t cnt;
+        if (find_cg(aux, rend, &arr, &cnt) && cnt >= n_cig && cnt < (1u << 29)) { v.cig = arr; v.n = cnt; v.cg = true; }
+    }
+    // Soft-clip test words as the reference reads them through bam1_t.data: the qname is
+    // padded with NULs to a multiple of 4 (htslib l_extranul), so cigar[-1] is the last 4
+    // bytes of the padded name and cigar[0] of an empty CIGAR is the first SEQ byte.
+    uint8_t c = 0;
+    if (v.n) {
+        if ((rd32(v.cig + 4ull * (v.n - 1)) & 0xfu) == OP_S) c |= SVT_CLIP_LAST_S;
+        if ((rd32(v.cig) & 0xfu) == OP_S) c |= SVT_CLIP_FIRST_S;
+    } else {
+        uint32_t padded = (l_qname + 3u) & ~3u;
+        uint8_t lastw0 = (padded >= 4 && padded - 4 < l_qname) ? qn[padded - 4] : 0;
+        if ((lastw0 & 0xfu) == OP_S) c |= SVT_CLIP_LAST_S;
+        if (after < rend && (after[0] & 0xfu) == OP_S) c |= SVT_CLIP_FIRST_S;
+    }
+    v.clip = c;
+    return v;
+}
+
+// Growable array without value-initialisation; large blocks grow by realloc (mremap on
+// glibc), so appending a chunk never re-copies or zero-fills what is already there.
+template <typename T>
+struct RawVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    RawVec() = default;
+    RawVec(const RawVec &) = delete;
+    RawVec &operator=(const RawVec &) = delete;
+    ~RawVec() { free(p); }
+    bool resize(size_t m) {
+        if (m > cap) {
+            size_t c = std::max(m, cap + cap / 2 + 1024);
+            T *q = (T *)realloc(p, c * sizeof(T));
+            if (!q) return false;
+            p = q;
+            cap = c;
+        }
+        n = m;
+        return true;
+    }
+    bool push_back(T v) {
+        if (!resize(n + 1)) return false;
+        p[n - 1] = v;
+        return true;
+    }
+    size_t size() const { return n; }
+    T *data() { return p; }
+    const T *data() const { return p; }
+    T &operator[](size_t i) { return p[i]; }
+    const T &operator[](size_t i) const { return p[i]; }
+    void swap(RawVec &o) { std::swap(p, o.p); std::swap(n, o.n); std::swap(cap, o.cap); }
+};
+
 }  // namespace
+
+struct svth_bam {
+    std::vector<std::string> names;
+    std::vector<int64_t> tid_off;
+    RawVec<int32_t> pos, endpos;
+    RawVec<uint64_t> cig_off;
+    RawVec<uint32_t> cigar;
+    RawVec<uint8_t> clip;
+    int64_t n_records = 0, n_cg = 0;
+};
 
 extern "C" {
 
@@ -184,110 +311,136 @@ svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap)
     size_t at = 0;
     auto need = [&](size_t k) -> bool {
         while (buf.size() - at < k) {
-            if (at > (16u << 20)) { buf.erase(buf.begin(), buf.begin() + (ptrdiff_t)at); at = 0; }
+            if (at) { buf.erase(buf.begin(), buf.begin() + (ptrdiff_t)at); at = 0; }
             if (!rd.next(buf)) return false;
         }
         return true;
     };
     svth_bam *b = new svth_bam();
+    auto bail = [&](const std::string &m) { fclose(f); delete b; return fail(rd.err.empty() ? m : rd.err); };
     // header
-    if (!need(8) || memcmp(buf.data() + at, "BAM\1", 4) != 0) {
-        fclose(f); delete b;
-        return fail(rd.err.empty() ? "not a BAM file" : rd.err);
-    }
-    uint32_t l_text = rd32(buf.data() + at + 4);
+    if (!need(8) || memcmp(buf.data() + at, "BAM\1", 4) != 0) return bail("not a BAM file");
+    const uint32_t l_text = rd32(buf.data() + at + 4);
     at += 8;
-    if (!need((size_t)l_text + 4)) { fclose(f); delete b; return fail("truncated BAM header"); }
+    if (!need((size_t)l_text + 4)) return bail("truncated BAM header");
     at += l_text;
-    int32_t n_ref = (int32_t)rd32(buf.data() + at);
+    const int32_t n_ref = (int32_t)rd32(buf.data() + at);
     at += 4;
-    if (n_ref < 0) { fclose(f); delete b; return fail("bad n_ref"); }
+    if (n_ref < 0) return bail("bad n_ref");
     for (int32_t i = 0; i < n_ref; i++) {
-        if (!need(4)) { fclose(f); delete b; return fail("truncated reference list"); }
-        uint32_t ln = rd32(buf.data() + at);
-        if (!need(4 + (size_t)ln + 4)) { fclose(f); delete b; return fail("truncated reference list"); }
+        if (!need(4)) return bail("truncated reference list");
+        const uint32_t ln = rd32(buf.data() + at);
+        if (!need(4 + (size_t)ln + 4)) return bail("truncated reference list");
         b->names.emplace_back((const char *)buf.data() + at + 4, ln ? ln - 1 : 0);
         at += 4 + ln + 4;
     }
-    std::vector<RawRead> rr;
-    std::vector<uint32_t> arena;
-    int64_t seq = 0;
+    // records, chunk by chunk
+    RawVec<int32_t> tid_of;
+    std::vector<uint8_t> rec_ok;
+    std::vector<uint16_t> flag;
+    uint64_t narena = 0;
+    std::vector<size_t> roff;
+    std::vector<uint32_t> rlen;
+    std::vector<RecView> views;
     for (;;) {
         if (buf.size() - at < 4 && !need(4)) break;   // clean EOF
-        uint32_t bs = rd32(buf.data() + at);
-        if (bs < 32) { fclose(f); delete b; return fail("corrupt BAM record (block_size < 32)"); }
-        if (!need(4 + (size_t)bs)) { fclose(f); delete b; return fail(rd.err.empty() ? "truncated BAM record" : rd.err); }
-        const uint8_t *r = buf.data() + at + 4, *rend = r + bs;
-        at += 4 + bs;
-        b->n_records++;
-        int32_t tid = (int32_t)rd32(r), pos = (int32_t)rd32(r + 4);
-        uint32_t l_qname = r[8];
-        uint16_t n_cig = rd16(r + 12), flag = rd16(r + 14);
-        int32_t l_seq = (int32_t)rd32(r + 16);
-        if (tid < 0 || tid >= n_ref) continue;      // never yielded by a tid >= 0 region query
-        const uint8_t *qn = r + 32, *cg = qn + l_qname;
-        if (cg + 4ull * n_cig > rend || l_seq < 0) { fclose(f); delete b; return fail("corrupt BAM record"); }
-        const uint8_t *after = cg + 4ull * n_cig;    // SEQ starts here
-        const uint8_t *aux = after + (size_t)(l_seq + 1) / 2 + (size_t)l_seq;
-        const uint8_t *src = cg;
-        uint32_t n = n_cig;
-        if (n_cig > 0 && pos >= 0 && (rd32(cg) & 0xfu) == OP_S && (int64_t)(rd32(cg) >> 4) == l_seq && aux <= rend) {
-            const uint8_t *arr;
-            uint32_t cnt;
-            if (find_cg(aux, rend, &arr, &cnt) && cnt >= n_cig && cnt < (1u << 29)) {
-                src = arr; n = cnt; b->n_cg++;
-            }
+        // sequential boundary scan over the complete records in the buffer
+        roff.clear();
+        size_t p = at;
+        while (buf.size() - p >= 4) {
+            const uint32_t bs = rd32(buf.data() + p);
+            if (bs < 32) return bail("corrupt BAM record (block_size < 32)");
+            if (buf.size() - p < 4 + (size_t)bs) break;
+            roff.push_back(p + 4);
+            p += 4 + bs;
         }
-        RawRead x;
-        x.tid = tid; x.pos = pos; x.off = arena.size(); x.n = n; x.seq = seq++;
-        arena.resize(arena.size() + n);
-        if (n) memcpy(arena.data() + x.off, src, 4ull * n);
-        int64_t rl = 0;
-        if (!(flag & 4))
-            for (uint32_t i = 0; i < n; i++) {
-                uint32_t op = arena[x.off + i] & 0xfu;
-                if (op == OP_M || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X) rl += arena[x.off + i] >> 4;
-            }
-        x.endpos = (int32_t)(pos + (rl ? rl : 1));
-        // Soft-clip test words as the reference reads them through bam1_t.data: the qname is
-        // padded with NULs to a multiple of 4 (htslib l_extranul), so cigar[-1] is the last
-        // 4 bytes of the padded name and cigar[0] of an empty CIGAR is the first SEQ byte.
-        uint8_t c = 0;
-        if (n) {
-            if ((arena[x.off + n - 1] & 0xfu) == OP_S) c |= SVT_CLIP_LAST_S;
-            if ((arena[x.off] & 0xfu) == OP_S) c |= SVT_CLIP_FIRST_S;
-        } else {
-            uint32_t padded = (l_qname + 3u) & ~3u;
-            uint8_t lastw0 = padded >= 4 ? (padded - 4 < l_qname ? qn[padded - 4] : 0) : 0;
-            if ((lastw0 & 0xfu) == OP_S) c |= SVT_CLIP_LAST_S;
-            if (after < rend && (after[0] & 0xfu) == OP_S) c |= SVT_CLIP_FIRST_S;
+        if (roff.empty()) {   // one record larger than the buffer: read on
+            if (!need(4 + (size_t)rd32(buf.data() + at))) return bail("truncated BAM record");
+            continue;
         }
-        x.clip = c;
-        if (pos < 0) continue;
-        rr.push_back(x);
+        // pass 1 (parallel): locate every record's CIGAR
+        const size_t nr = roff.size();
+        views.resize(nr);
+        parallel_for(rd.threads, nr, [&](size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; i++)
+                views[i] = view_record(buf.data() + roff[i], rd32(buf.data() + roff[i] - 4), n_ref);
+        });
+        // prefix offsets, then pass 2 (parallel): copy into the columnar arrays
+        const size_t base = b->pos.size();
+        size_t kept = 0;
+        for (size_t i = 0; i < nr; i++) {
+            if (views[i].n == 0xffffffffu) return bail("corrupt BAM record");
+            if (views[i].ok) kept++;
+            if (views[i].cg) b->n_cg++;
+        }
+        b->n_records += (int64_t)nr;
+        std::vector<uint64_t> off(nr + 1, 0);
+        std::vector<size_t> slot(nr, 0);
+        for (size_t i = 0, k = base; i < nr; i++) {
+            off[i + 1] = off[i] + (views[i].ok ? views[i].n : 0);
+            slot[i] = views[i].ok ? k++ : (size_t)-1;
+        }
+        if (!b->pos.resize(base + kept) || !b->endpos.resize(base + kept) || !b->clip.resize(base + kept) ||
+            !tid_of.resize(base + kept) || !b->cig_off.resize(base + kept) || !b->cigar.resize(narena + off[nr]))
+            return bail("out of host memory");
+        parallel_for(rd.threads, nr, [&](size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; i++) {
+                const RecView &v = views[i];
+                if (!v.ok) continue;
+                const size_t k = slot[i];
+                uint32_t *dst = b->cigar.data() + narena + off[i];
+                if (v.n) memcpy(dst, v.cig, 4ull * v.n);
+                int64_t rl = 0;
+                if (!(v.flag & 4))
+                    for (uint32_t j = 0; j < v.n; j++) {
+                        const uint32_t op = dst[j] & 0xfu;
+                        if (op == OP_M || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X) rl += dst[j] >> 4;
+                    }
+                b->pos[k] = v.pos;
+                b->endpos[k] = (int32_t)(v.pos + (rl ? rl : 1));   // htslib bam_endpos
+                b->clip[k] = v.clip;
+                b->cig_off[k] = narena + off[i];
+                tid_of[k] = v.tid;
+            }
+        });
+        narena += off[nr];
+        at = p;
     }
     fclose(f);
     if (!rd.err.empty()) { delete b; return fail(rd.err); }
-    // columnar, per tid sorted by pos (file order among equal pos; order is irrelevant)
-    std::vector<size_t> idx(rr.size());
-    std::iota(idx.begin(), idx.end(), 0);
-    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t c) {
-        return rr[a].tid != rr[c].tid ? rr[a].tid < rr[c].tid : rr[a].pos < rr[c].pos;
-    });
-    b->tid_off.assign((size_t)n_ref + 1, 0);
-    b->pos.resize(rr.size()); b->endpos.resize(rr.size()); b->clip.resize(rr.size());
-    b->cig_off.resize(rr.size() + 1);
-    b->cigar.resize(arena.size());
-    uint64_t w = 0;
-    for (size_t k = 0; k < idx.size(); k++) {
-        const RawRead &x = rr[idx[k]];
-        b->tid_off[(size_t)x.tid + 1]++;
-        b->pos[k] = x.pos; b->endpos[k] = x.endpos; b->clip[k] = x.clip;
-        b->cig_off[k] = w;
-        if (x.n) memcpy(b->cigar.data() + w, arena.data() + x.off, 4ull * x.n);
-        w += x.n;
+    const size_t n = b->pos.size();
+    if (!b->cig_off.push_back(narena)) { delete b; return fail("out of host memory"); }
+    // per-tid ranges; reorder only when the file was not coordinate-sorted
+    bool sorted = true;
+    for (size_t i = 1; i < n && sorted; i++)
+        sorted = tid_of[i] > tid_of[i - 1] || (tid_of[i] == tid_of[i - 1] && b->pos[i] >= b->pos[i - 1]);
+    if (!sorted) {
+        std::vector<size_t> idx(n);
+        std::iota(idx.begin(), idx.end(), 0);
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
+            return tid_of[x] != tid_of[y] ? tid_of[x] < tid_of[y] : b->pos[x] < b->pos[y];
+        });
+        RawVec<int32_t> pos2, end2, tid2;
+        RawVec<uint8_t> clip2;
+        RawVec<uint64_t> off2;
+        RawVec<uint32_t> cig2;
+        if (!pos2.resize(n) || !end2.resize(n) || !tid2.resize(n) || !clip2.resize(n) || !off2.resize(n + 1) ||
+            !cig2.resize(narena)) { delete b; return fail("out of host memory"); }
+        uint64_t w = 0;
+        for (size_t k = 0; k < n; k++) {
+            const size_t i = idx[k];
+            pos2[k] = b->pos[i]; end2[k] = b->endpos[i]; clip2[k] = b->clip[i]; tid2[k] = tid_of[i];
+            const uint64_t o = b->cig_off[i], m = b->cig_off[i + 1] - o;
+            off2[k] = w;
+            if (m) memcpy(cig2.data() + w, b->cigar.data() + o, 4 * m);
+            w += m;
+        }
+        off2[n] = w;
+        b->pos.swap(pos2); b->endpos.swap(end2); b->clip.swap(clip2); b->cig_off.swap(off2); b->cigar.swap(cig2);
+        tid_of.swap(tid2);
     }
-    b->cig_off[rr.size()] = w;
+    b->tid_off.assign((size_t)n_ref + 1, 0);
+    for (size_t k = 0; k < n; k++) b->tid_off[(size_t)tid_of[k] + 1]++;
     for (int32_t t = 0; t < n_ref; t++) b->tid_off[(size_t)t + 1] += b->tid_off[(size_t)t];
     return b;
 }
