@@ -35,7 +35,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.5.0 (gfx950, window-stream kernel, 4 waves per window)"
+#define SVT_VERSION "svtrek_amd 0.4.1 (gfx950, window-stream kernel)"
 
 namespace {
 
@@ -90,8 +90,9 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ int32_t uniform_i(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-// Wave-local ordering (a wave's own LDS/global hand-offs between its lanes): a
-// workgroup-scope release/acquire pair around a wave barrier, no s_barrier.
+// Every window is owned by ONE wave (several independent waves share a workgroup), so the
+// only ordering ever needed is between the lanes of a wave: a workgroup-scope
+// release/acquire pair around a wave barrier (no s_barrier across the workgroup).
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -278,35 +279,12 @@ __device__ __forceinline__ bool read_range(const DevPileup &P, int tid, int64_t 
     return lo < hi;
 }
 
-// The yielded reads of a window are split evenly over the waves of its workgroup: part p
-// of n takes reads [lo + m*p/n, lo + m*(p+1)/n), m = hi - lo (candidates are a multiset).
-#ifndef SVT_SPLIT_BY_OPS
-#define SVT_SPLIT_BY_OPS 0
-#endif
-__device__ __forceinline__ bool split_range(int64_t &lo, int64_t &hi, int part, int nparts, const uint64_t *off64) {
-    const int64_t m = hi - lo, l0 = lo, h0 = hi;
-    if (!SVT_SPLIT_BY_OPS || nparts == 1 || m <= nparts) {
-        lo = l0 + m * part / nparts;
-        hi = l0 + m * (part + 1) / nparts;
-        return lo < hi;
-    }
-    // equal shares of the window's CIGAR span: part p starts at the first read whose
-    // padded offset reaches S0 + span*p/n
-    const uint64_t a0 = off64[l0], span = off64[h0] - a0;
-    const uint64_t t0 = a0 + span * (uint64_t)part / (uint64_t)nparts;
-    const uint64_t t1 = a0 + span * (uint64_t)(part + 1) / (uint64_t)nparts;
-    lo = part == 0 ? l0 : wave_partition_point(l0, h0, [&](int64_t r) { return off64[r] >= t0; });
-    hi = part == nparts - 1 ? h0 : wave_partition_point(l0, h0, [&](int64_t r) { return off64[r] >= t1; });
-    return lo < hi;
-}
-
 // ------------------------------------------------------------------ per-read gather (v1)
 template <int KIND, bool COUNT>
-__device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
-                                               int part, int nparts) {
+__device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi) || !split_range(lo, hi, part, nparts, P.off64)) return;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
     const int ln = lane_id();
     for (int64_t base = lo; base < hi; base += WAVE) {
         int64_t r = base + ln;
@@ -348,13 +326,13 @@ struct StreamLds {
 
 template <int KIND, bool COUNT>
 __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
-                                              WinStats &st, StreamLds &L, int part, int nparts) {
+                                              WinStats &st, StreamLds &L) {
     // Positions in the stream stay below 2^32 (no wrap) when inter.end < 2^31 and every
     // streamed read walks less than 2^31 (the others are flagged slow at load time).
-    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st, part, nparts); return; }
+    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi) || !split_range(lo, hi, part, nparts, P.off64)) return;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
     const int ln = lane_id();
     const uint64_t S0 = P.off64[lo];
     const uint32_t base32 = (uint32_t)S0;
@@ -654,108 +632,115 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
     return vote(buf, P, n, pos, k);
 }
 
-// One workgroup per query window: its WPB waves split the window's yielded reads
-// (split_range), append candidates to one LDS buffer, meet at ONE workgroup barrier, and
-// wave 0 sorts + votes.  Windows g < n are each locus' first window (DEL: refine_start
-// over [pos-wider, pos+narrow]; INS: refine_ins), n + i locus i's second (DEL:
-// refine_end over end +- narrow): the wide windows are dispatched first.
-constexpr int WPB = 4;
-
-struct WgLds {
-    union {                         // the per-wave stream scratch is dead once the vote starts
-        StreamLds sl[WPB];
+struct WinLds {
+    union {                       // the stream scratch is dead once the vote starts
+        StreamLds sl;
         int64_t pre[CAP + 1];
     };
     int32_t cand[CAP];
     int32_t ncand;
-    unsigned long long slab;        // spill slab base (broadcast by wave 0), or ~0 on exhaustion
 };
 
 template <int KIND, bool COUNT, bool STREAM>
-__device__ __forceinline__ void gather_part(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
-                                            StreamLds &L, int part) {
-    if (STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L, part, WPB);
-    else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st, part, WPB);
+__device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
+                                          StreamLds &L) {
+    if (lane_id() == 0) *sink.cnt = 0;
+    wave_sync();
+    if (STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L);
+    else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    wave_sync();
+    return uniform_i(*sink.cnt);
 }
 
-// Returns the vote (valid in wave 0 only).
 template <int KIND, bool COUNT, bool STREAM>
-__device__ __forceinline__ int32_t refine_window(const KArgs &a, WgLds &lds, int wid, int chrom, uint32_t s, uint32_t e,
-                                                 uint32_t imprecise) {
+__device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e, uint32_t imprecise,
+                                 unsigned long long *wk) {
     WinStats st;
     Sink sink{lds.cand, CAP, &lds.ncand};
-    if (threadIdx.x == 0) lds.ncand = 0;
-    __syncthreads();
-    gather_part<KIND, COUNT, STREAM>(a, chrom - 1, s, e, sink, st, lds.sl[wid], wid);
-    __syncthreads();
-    const int32_t n = uniform_i(lds.ncand);
+    int32_t n = gather<KIND, COUNT, STREAM>(a, chrom - 1, s, e, sink, st, lds.sl);
     if (COUNT && lane_id() == 0) {
-        if (wid == 0) { atomicAdd(a.work + 0, 1ull); atomicAdd(a.work + 3, (unsigned long long)n); }
-        if (st.reads) atomicAdd(a.work + 1, st.reads);
-        if (st.ops) atomicAdd(a.work + 2, st.ops);
+        wk[0] += 1; wk[1] += st.reads; wk[2] += st.ops; wk[3] += (unsigned long long)n;
     }
     if (n < a.prm.min_count) return -1;                    // refinement.c:43-45
-    if (n <= CAP) {
-        if (wid != 0) return -1;
-        return sort_and_vote(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm);
-    }
+    if (n <= CAP) return sort_and_vote(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm);
     // spill: a slab for N ints + (n+1) int64 from the device pool, then re-gather into it
+    if (COUNT && lane_id() == 0) wk[4] += 1;
     int N = 1;
     while (N < n) N <<= 1;
-    const unsigned long long words = (unsigned long long)N + 2ull * (unsigned long long)(n + 2);
-    if (threadIdx.x == 0) {
-        if (COUNT) atomicAdd(a.work + 4, 1ull);
-        unsigned long long base = atomicAdd(a.pool_head, words);
-        if (base + words > a.pool_words) {
-            atomicOr(a.status, 1);
-            base = ~0ull;
-        }
-        lds.slab = base;
-        lds.ncand = 0;
+    unsigned long long words = (unsigned long long)N + 2ull * (unsigned long long)(n + 2);
+    unsigned long long base = 0;
+    if (lane_id() == 0) base = atomicAdd(a.pool_head, words);
+    base = rdlane64(base, 0);
+    if (base + words > a.pool_words) {
+        if (lane_id() == 0) atomicOr(a.status, 1);
+        return -1;
     }
-    __syncthreads();
-    const unsigned long long base = lds.slab;
-    if (base == ~0ull) return -1;
     int32_t *g = a.pool + base;
     int64_t *gp = (int64_t *)(a.pool + ((base + (unsigned long long)N + 1ull) & ~1ull));
     WinStats st2;
     Sink s2{g, N, &lds.ncand};
-    gather_part<KIND, false, STREAM>(a, chrom - 1, s, e, s2, st2, lds.sl[wid], wid);
-    __threadfence_block();
-    __syncthreads();
-    if (wid != 0) return -1;
+    gather<KIND, false, STREAM>(a, chrom - 1, s, e, s2, st2, lds.sl);
     return sort_and_vote(g, gp, n, (int32_t)imprecise, a.prm);
 }
 
+// One wave per query window, WPB independent waves per workgroup.  Window g < n is locus
+// g's first window (DEL: refine_start over [pos-wider, pos+narrow], INS: refine_ins),
+// window n + i is locus i's second (DEL: refine_end over end +- narrow): the wide windows
+// are dispatched first, so the short ones fill the tail.
+constexpr int WPB = 4;
+#ifndef SVT_INTERLEAVE_WINDOWS
+#define SVT_INTERLEAVE_WINDOWS 0
+#endif
+
 template <bool COUNT, bool STREAM>
-__global__ __launch_bounds__(64 * WPB) void refine_kernel(KArgs a) {
-    __shared__ WgLds lds;
-    const uint32_t g = blockIdx.x;
+#ifndef SVT_WAVES_PER_EU
+#define SVT_WAVES_PER_EU 0       // 0: let the compiler choose (70 VGPRs -> 7 waves/SIMD)
+#endif
+#if SVT_WAVES_PER_EU
+#define SVT_OCC __attribute__((amdgpu_waves_per_eu(SVT_WAVES_PER_EU, SVT_WAVES_PER_EU)))
+#else
+#define SVT_OCC
+#endif
+__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_kernel(KArgs a) {
+    __shared__ WinLds lds_all[WPB];
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x * WPB + wid;
     if (g >= 2 * a.n) return;
-    const int wid = (int)(threadIdx.x >> 6);
+    WinLds &lds = lds_all[wid];
+#if SVT_INTERLEAVE_WINDOWS
+    const uint32_t w = g & 1u, li = g >> 1;      // a locus' two windows back to back (L2/MALL reuse)
+#else
     const uint32_t w = g >= a.n ? 1u : 0u, li = g - w * a.n;
+#endif
     const svt_locus L = a.loci[li];
     const int32_t type = uniform_i(L.type), chrom = uniform_i(L.chrom);
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
+    unsigned long long wk[5] = {0, 0, 0, 0, 0};
     uint32_t r = SVT_NA;
     const KParams &k = a.prm;
     if (type == T_INS) {                                   // audit.c:176-187
         if (w == 0) {
             uint32_t s = pos - (uint32_t)k.median, e = pos + (uint32_t)k.median;
-            r = (uint32_t)refine_window<K_INS, COUNT, STREAM>(a, lds, wid, chrom, s, e, pos);
+            r = (uint32_t)refine_window<K_INS, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk);
         }
     } else if (type == T_DEL) {                            // audit.c:188-220
         if (w == 0) {
             uint32_t s = pos - (uint32_t)k.wider, e = pos + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_START, COUNT, STREAM>(a, lds, wid, chrom, s, e, pos);
+            r = (uint32_t)refine_window<K_START, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk);
         } else {
             uint32_t s = end - (uint32_t)k.narrow, e = end + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_END, COUNT, STREAM>(a, lds, wid, chrom, s, e, end);
+            r = (uint32_t)refine_window<K_END, COUNT, STREAM>(a, lds, chrom, s, e, end, wk);
         }
     }
     // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250), so both
     // windows vote on 0 candidates -> -1 for every min_count >= 1 (validated): NA, NA.
-    if (threadIdx.x == 0) reinterpret_cast<uint32_t *>(a.out + li)[w] = r;
+    if (lane_id() == 0) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(a.out + li);
+        o[w] = r;
+        if (COUNT)
+            for (int i = 0; i < 5; i++)
+                if (wk[i]) atomicAdd(a.work + i, wk[i]);
+    }
 }
 
 }  // namespace
@@ -835,7 +820,7 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     if (n > 0x3fffffffull) return fail(c, SVT_EINVAL, "batch too large (%s)", "n > 2^30-1");
     HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 64, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
-    dim3 grid((unsigned)(2 * n)), block(64 * WPB);
+    dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
     if (c->stream_gather) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, true>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((refine_kernel<false, true>), grid, block, 0, st, a);
