@@ -3,10 +3,12 @@
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         -m svtrek_amd.audt_dist -b sample.bam -v calls.vcf [--wider-interval N ...]
 
-Every rank reads the BAM into a columnar pileup and refines the contiguous VCF-row
-shard [r*ceil(N/G), (r+1)*ceil(N/G)) on its own GPU (svtrek_amd.Engine, HIP); rank 0
-gathers the 8-byte results (torch.distributed nccl = RCCL over xGMI) and prints the
-reference's stdout (A11) in VCF order.  Single-node `svtrek audt --gpus N` does the
+Every rank reads the BAM into a columnar pileup, takes the contiguous slice
+[r*ceil(N/G), (r+1)*ceil(N/G)) of the loci in genomic order, uploads only the reads its
+queries can reach (pileup.halo_slice) and refines them on its own GPU
+(svtrek_amd.Engine, HIP); rank 0 gathers the 16-byte {vcf_index, start, end, pad}
+records (torch.distributed nccl = RCCL over xGMI) and prints the reference's stdout
+(A11) in VCF order.  Single-node `svtrek audt --gpus N` does the
 same sharding with host threads instead of processes.
 """
 from __future__ import annotations
@@ -64,7 +66,8 @@ def main(argv=None) -> int:
     import torch.distributed as dist
 
     from . import Engine, Params, host
-    from .distributed import run_sharded
+    from .distributed import gather_results, shard_rows
+    from .pileup import halo_slice
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -83,10 +86,15 @@ def main(argv=None) -> int:
     prm = Params(a.wider_interval, a.median_interval, a.narrow_interval, a.consensus_interval_range,
                  a.consensus_interval, a.consensus_min_count)
     with Engine(prm, device=local) as eng:
-        eng.load_pileup(pileup)
         if world > 1:
-            res = run_sharded(loci, eng.refine, device=dev)
+            rows = shard_rows(loci, world, rank)
+            mine = loci[rows]
+            eng.load_pileup(halo_slice(pileup, mine, a.wider_interval, a.median_interval, a.narrow_interval))
+            del pileup
+            local_res = eng.refine(mine)
+            res = gather_results(rows, local_res, len(loci), device=dev)
         else:
+            eng.load_pileup(pileup)
             res = eng.refine(loci)
     if rank == 0:
         out = [host.format_result(loci[k], res[k]) for k in range(len(loci))]

@@ -6,11 +6,16 @@
 // records through its exit_signal race, SURVEY.md §3.1 -- not reproduced).  The work
 // between the two [INFO] lines is: read the BAM once into a columnar pileup (host,
 // -t inflate threads), copy it to HBM, parse all VCF records (A1), refine them in
-// batched HIP launches (svt_refine_batch; --gpus N shards records over N devices,
-// one host thread and one svt_ctx per device), print (A11).
+// batched HIP launches (svt_refine_batch; --gpus N puts the records in genomic order,
+// gives device g the g-th contiguous slice and uploads only the reads that slice's
+// queries can reach; one host thread and one svt_ctx per device),
+// print (A11).
 #include <getopt.h>
 
+#include <algorithm>
 #include <chrono>
+#include <climits>
+#include <numeric>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -48,6 +53,7 @@ void audt_usage() {
     printf("GPU options (svtrek_amd):\n");
     printf("    --gpus <num>                      GPUs to shard records over [Default: 1]\n");
     printf("    --device <num>                    First GPU index [Default: 0]\n");
+    printf("    --devices <i,j,...>               Explicit GPU per shard (overrides --gpus/--device)\n");
     printf("    --batch <num>                     Records per GPU launch [Default: 1048576]\n");
 }
 
@@ -55,6 +61,7 @@ struct Args {
     const char *bam = nullptr, *vcf = nullptr, *out = "svtrek.out";
     int threads = THREADS, verbose = 0, gpus = 1, device = 0;
     size_t batch = 1u << 20;
+    std::vector<int> devices;   // device of shard g
     svt_params prm{WIDER, MEDIAN, NARROW, CI_RANGE, CI, MIN_COUNT, 0};
 };
 
@@ -86,7 +93,7 @@ Args parse_audt(int argc, char **argv) {
         {"consensus-interval", required_argument, nullptr, 9},
         {"consensus-min-count", required_argument, nullptr, 10}, {"help", no_argument, nullptr, 11},
         {"gpus", required_argument, nullptr, 20}, {"device", required_argument, nullptr, 21},
-        {"batch", required_argument, nullptr, 22}, {nullptr, 0, nullptr, 0}};
+        {"batch", required_argument, nullptr, 22}, {"devices", required_argument, nullptr, 23}, {nullptr, 0, nullptr, 0}};
     int opt, li;
     while ((opt = getopt_long(argc, argv, "b:v:o:t:h", opts, &li)) != -1) {
         switch (opt) {
@@ -105,6 +112,18 @@ Args parse_audt(int argc, char **argv) {
         case 20: a.gpus = atoi(optarg); break;
         case 21: a.device = atoi(optarg); break;
         case 22: a.batch = (size_t)strtoull(optarg, nullptr, 10); break;
+        case 23: {
+            a.devices.clear();
+            for (const char *p = optarg; *p;) {
+                char *e;
+                long d = strtol(p, &e, 10);
+                if (e == p || d < 0) { fprintf(stderr, "[ERROR] --devices expects a list like 0,1,2\n"); exit(EXIT_FAILURE); }
+                a.devices.push_back((int)d);
+                p = *e == ',' ? e + 1 : e;
+                if (*e && *e != ',') { fprintf(stderr, "[ERROR] --devices expects a list like 0,1,2\n"); exit(EXIT_FAILURE); }
+            }
+            break;
+        }
         default:
             printf("[ERROR] Option %d is invalid.\n", opt);
             audt_usage();
@@ -118,6 +137,9 @@ Args parse_audt(int argc, char **argv) {
     if (a.prm.consensus_min_count < 1) { fprintf(stderr, "[ERROR] --consensus-min-count must be >= 1\n"); exit(EXIT_FAILURE); }
     if (a.gpus < 1) a.gpus = 1;
     if (a.batch < 1) a.batch = 1;
+    if (a.devices.empty())
+        for (int g = 0; g < a.gpus; g++) a.devices.push_back(a.device + g);
+    a.gpus = (int)a.devices.size();
     return a;
 }
 
@@ -133,6 +155,72 @@ bool read_file(const char *path, std::string &s) {
 
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// One device's genomic shard: its loci (genomic order, VCF rows kept) and a copy of the
+// reads their queries can yield.  Query hull per contig: A2 windows in uint32
+// (audit.c:178,191-192), sam_itr_queryi(start-1, end-1) (refinement.c:114), empty when
+// end <= beg; INV collects nothing (A7).  A read is kept when pos < hull.end and
+// endpos > hull.beg -- a superset of every query's yield, so results are unchanged.
+struct Shard {
+    std::vector<size_t> rows;
+    std::vector<svt_locus> loci;
+    std::vector<svt_result> res;
+    std::vector<int64_t> tid_off;
+    std::vector<int32_t> pos, endpos;
+    std::vector<uint64_t> cig_off;
+    std::vector<uint32_t> cigar;
+    std::vector<uint8_t> clip;
+    svt_pileup_view view{};
+};
+
+void build_shard(const svt_pileup_view &full, const std::vector<svt_locus> &loci, const std::vector<size_t> &rows,
+                 const svt_params &prm, Shard &sh) {
+    sh.rows = rows;
+    sh.loci.resize(rows.size());
+    for (size_t k = 0; k < rows.size(); k++) sh.loci[k] = loci[rows[k]];
+    sh.res.resize(rows.size());
+    const int nt = full.n_targets;
+    std::vector<int64_t> lo(nt, INT64_MAX), hi(nt, INT64_MIN);
+    auto add = [&](const svt_locus &l, uint32_t s, uint32_t e) {
+        int64_t b = (uint32_t)(s - 1u), q = (uint32_t)(e - 1u);
+        int tid = l.chrom - 1;
+        if (q <= b || tid < 0 || tid >= nt) return;
+        lo[tid] = std::min(lo[tid], b);
+        hi[tid] = std::max(hi[tid], q);
+    };
+    for (const svt_locus &l : sh.loci) {
+        if (l.type == 1) add(l, l.pos - (uint32_t)prm.median_interval, l.pos + (uint32_t)prm.median_interval);
+        if (l.type == 2) {
+            add(l, l.pos - (uint32_t)prm.wider_interval, l.pos + (uint32_t)prm.narrow_interval);
+            add(l, l.end - (uint32_t)prm.narrow_interval, l.end + (uint32_t)prm.narrow_interval);
+        }
+    }
+    sh.tid_off.assign(1, 0);
+    sh.cig_off.assign(1, 0);
+    for (int t = 0; t < nt; t++) {
+        int64_t a = full.tid_off[t], b = full.tid_off[t + 1];
+        if (hi[t] > lo[t]) {
+            const int32_t *cut = std::lower_bound(full.pos + a, full.pos + b, hi[t],
+                                                  [](int32_t p, int64_t v) { return (int64_t)p < v; });
+            for (int64_t r = a; r < cut - full.pos; r++) {
+                if ((int64_t)full.endpos[r] <= lo[t]) continue;
+                sh.pos.push_back(full.pos[r]);
+                sh.endpos.push_back(full.endpos[r]);
+                if (full.clip) sh.clip.push_back(full.clip[r]);
+                sh.cigar.insert(sh.cigar.end(), full.cigar + full.cig_off[r], full.cigar + full.cig_off[r + 1]);
+                sh.cig_off.push_back(sh.cigar.size());
+            }
+        }
+        sh.tid_off.push_back((int64_t)sh.pos.size());
+    }
+    sh.view.n_targets = nt;
+    sh.view.tid_off = sh.tid_off.data();
+    sh.view.pos = sh.pos.data();
+    sh.view.endpos = sh.endpos.data();
+    sh.view.cig_off = sh.cig_off.data();
+    sh.view.cigar = sh.cigar.data();
+    sh.view.clip = full.clip ? sh.clip.data() : nullptr;
 }
 
 int audit(int argc, char **argv) {
@@ -177,19 +265,40 @@ int audit(int argc, char **argv) {
     const int G = a.gpus;
     std::vector<int> rc(G, 0);
     std::vector<std::string> gerr(G);
+    std::vector<size_t> order;
+    if (G > 1) {
+        order.resize(loci.size());
+        std::iota(order.begin(), order.end(), (size_t)0);
+        std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+            return loci[x].chrom != loci[y].chrom ? loci[x].chrom < loci[y].chrom : loci[x].pos < loci[y].pos;
+        });
+    }
     auto worker = [&](int g) {
-        size_t n = loci.size(), per = (n + G - 1) / G;
-        size_t b0 = std::min(n, per * (size_t)g), b1 = std::min(n, b0 + per);
         svt_ctx *ctx = nullptr;
-        int s = svt_open(&a.prm, a.device + g, &ctx);
+        int s = svt_open(&a.prm, a.devices[g], &ctx);
         if (s) { rc[g] = s; gerr[g] = "svt_open failed (HIP device?)"; return; }
-        s = svt_load_pileup(ctx, &view);
-        for (size_t k = b0; !s && k < b1; k += a.batch) {
-            size_t m = std::min(a.batch, b1 - k);
-            s = svt_refine_batch(ctx, loci.data() + k, m, res.data() + k);
+        const svt_locus *in = loci.data();
+        svt_result *out = res.data();
+        size_t n = loci.size();
+        Shard sh;
+        if (G > 1) {
+            size_t per = (n + G - 1) / G, b0 = std::min(n, per * (size_t)g), b1 = std::min(n, b0 + per);
+            build_shard(view, loci, std::vector<size_t>(order.begin() + b0, order.begin() + b1), a.prm, sh);
+            s = svt_load_pileup(ctx, &sh.view);
+            in = sh.loci.data();
+            out = sh.res.data();
+            n = sh.loci.size();
+        } else {
+            s = svt_load_pileup(ctx, &view);
+        }
+        for (size_t k = 0; !s && k < n; k += a.batch) {
+            size_t m = std::min(a.batch, n - k);
+            s = svt_refine_batch(ctx, in + k, m, out + k);
         }
         if (s) { rc[g] = s; gerr[g] = svt_last_error(ctx); }
         svt_close(ctx);
+        if (!s && G > 1)
+            for (size_t k = 0; k < sh.rows.size(); k++) res[sh.rows[k]] = sh.res[k];
     };
     if (G == 1) worker(0);
     else {
@@ -198,7 +307,7 @@ int audit(int argc, char **argv) {
         for (auto &t : th) t.join();
     }
     for (int g = 0; g < G; g++)
-        if (rc[g]) { fprintf(stderr, "[ERROR] GPU %d: %s (status %d)\n", a.device + g, gerr[g].c_str(), rc[g]); return 1; }
+        if (rc[g]) { fprintf(stderr, "[ERROR] GPU %d: %s (status %d)\n", a.devices[g], gerr[g].c_str(), rc[g]); return 1; }
     svth_bam_free(bam);
     const double t_refine = now_s();
 

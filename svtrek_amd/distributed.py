@@ -1,10 +1,12 @@
 """Multi-GPU sharding of SV loci: one process per GPU, one gather of refined calls.
 
 SURVEY.md §8(e): records are independent (reference thread_func keeps no cross-record
-state, audit.c:50-248), so rank g refines the contiguous row range
-[g*ceil(N/G), (g+1)*ceil(N/G)) and the only collective is ONE gather of the fixed-size
-results to rank 0 (RCCL over xGMI with the nccl backend; gloo on CPU for tests).
-Results travel as uint32 pairs padded to ceil(N/G) rows with 0xFFFFFFFF.
+state, audit.c:50-248).  Loci are put in genomic order (tid, pos) keeping their VCF row
+index, rank g refines the contiguous range [g*ceil(N/G), (g+1)*ceil(N/G)) of that order
+against only the reads its queries can reach (pileup.halo_slice), and the only collective
+is ONE gather to rank 0 of fixed-size {uint32 vcf_index, start, end, pad} records (RCCL
+over xGMI with the nccl backend; gloo on CPU for tests), padded to ceil(N/G) rows with
+vcf_index 0xFFFFFFFF.  Rank 0 scatters the records back into VCF order.
 """
 from __future__ import annotations
 
@@ -14,6 +16,8 @@ import numpy as np
 
 from ._lib import RESULT_DTYPE, SVT_NA
 
+PAD_INDEX = 0xFFFFFFFF
+
 
 def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     per = (n + world - 1) // world if world > 0 else n
@@ -21,37 +25,71 @@ def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     return b0, min(n, b0 + per)
 
 
-def gather_results(local: np.ndarray, n_total: int, device=None, group=None) -> np.ndarray | None:
-    """Gather every rank's RESULT_DTYPE rows to rank 0 (rows in rank order)."""
+def genomic_order(loci: np.ndarray) -> np.ndarray:
+    """VCF row indices sorted by (chrom, pos), stable (ties keep VCF order)."""
+    return np.lexsort((loci["pos"], loci["chrom"])).astype(np.int64)
+
+
+def shard_rows(loci: np.ndarray, world: int, rank: int) -> np.ndarray:
+    """The VCF row indices rank `rank` refines: a contiguous slice of the genomic order."""
+    b0, b1 = shard_bounds(len(loci), world, rank)
+    return genomic_order(loci)[b0:b1]
+
+
+def pack_records(rows: np.ndarray, local: np.ndarray, per: int) -> np.ndarray:
+    """{vcf_index, start, end, pad} uint32 records, padded to `per` rows."""
+    if len(rows) > per:
+        raise ValueError(f"shard of {len(rows)} rows exceeds the padded size {per}")
+    buf = np.full((per, 4), SVT_NA, dtype=np.uint32)
+    buf[:, 0] = PAD_INDEX
+    buf[:len(rows), 0] = rows
+    buf[:len(rows), 1] = local["start"]
+    buf[:len(rows), 2] = local["end"]
+    buf[:, 3] = 0
+    return buf
+
+
+def unpack_records(recs: np.ndarray, n_total: int) -> np.ndarray:
+    """Scatter gathered records into VCF order; every row must arrive exactly once."""
+    recs = recs.reshape(-1, 4)
+    real = recs[recs[:, 0] != PAD_INDEX]
+    idx = real[:, 0].astype(np.int64)
+    if len(idx) != n_total or (n_total and (idx.max() >= n_total or np.bincount(idx, minlength=n_total).max() != 1)):
+        raise RuntimeError("gathered records do not cover every VCF row exactly once")
+    out = np.empty(n_total, dtype=RESULT_DTYPE)
+    out["start"][idx] = real[:, 1]
+    out["end"][idx] = real[:, 2]
+    return out
+
+
+def gather_results(rows: np.ndarray, local: np.ndarray, n_total: int, device=None,
+                   group=None) -> np.ndarray | None:
+    """Gather every rank's (rows, results) to rank 0 and return all results in VCF order."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    per = (n_total + world - 1) // world
-    buf = np.full((per, 2), SVT_NA, dtype=np.uint32)
-    if len(local):
-        buf[:len(local), 0] = local["start"]
-        buf[:len(local), 1] = local["end"]
-    t = torch.from_numpy(buf.view(np.int32).copy())
+    per = max(1, (n_total + world - 1) // world)
+    t = torch.from_numpy(pack_records(rows, local, per).view(np.int32).copy())
     if device is not None:
         t = t.to(device)
     parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
     dist.gather(t, parts, dst=0, group=group)
     if rank != 0:
         return None
-    allrows = np.concatenate([p.cpu().numpy().view(np.uint32) for p in parts])[:n_total]
-    out = np.empty(n_total, dtype=RESULT_DTYPE)
-    out["start"] = allrows[:, 0]
-    out["end"] = allrows[:, 1]
-    return out
+    allrecs = np.concatenate([p.cpu().numpy().view(np.uint32) for p in parts])
+    return unpack_records(allrecs, n_total)
 
 
 def run_sharded(loci: np.ndarray, refine: Callable[[np.ndarray], np.ndarray], device=None,
                 group=None) -> np.ndarray | None:
-    """Refine this rank's shard with `refine` and gather all results to rank 0."""
+    """Refine this rank's genomic shard with `refine(loci_subset)` and gather to rank 0.
+
+    `refine` sees the shard's loci in genomic order; callers that hold a pileup give it
+    `pileup.halo_slice(full, shard_loci, ...)` first (see audt_dist)."""
     import torch.distributed as dist
 
-    b0, b1 = shard_bounds(len(loci), dist.get_world_size(group), dist.get_rank(group))
-    local = refine(loci[b0:b1]) if b1 > b0 else np.zeros(0, dtype=RESULT_DTYPE)
-    return gather_results(local, len(loci), device=device, group=group)
+    rows = shard_rows(loci, dist.get_world_size(group), dist.get_rank(group))
+    local = refine(loci[rows]) if len(rows) else np.zeros(0, dtype=RESULT_DTYPE)
+    return gather_results(rows, local, len(loci), device=device, group=group)

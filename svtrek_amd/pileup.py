@@ -115,3 +115,65 @@ def make_loci(rows) -> np.ndarray:
     for i, (t, c, p, e) in enumerate(rows):
         a[i] = (t, c, p & 0xFFFFFFFF, e & 0xFFFFFFFF)
     return a
+
+
+def query_spans(loci: np.ndarray, wider: int, median: int, narrow: int, n_targets: int) -> np.ndarray:
+    """Per contig, the [beg, end) hull of every htslib query the loci issue (int64 [n_targets, 2];
+    beg > end when the contig has none).
+
+    Windows are A2 (audit.c:178 INS, :191-192 DEL) in uint32 with wrap-around and the query
+    bounds are sam_itr_queryi(start-1, end-1) (refinement.c:114); an empty query (end <= beg)
+    or a tid outside the header yields nothing.  INV never collects (A7), so it adds no span.
+    """
+    M = np.uint64(0xFFFFFFFF)
+    t = loci["type"]
+    pos = loci["pos"].astype(np.uint64)
+    end = loci["end"].astype(np.uint64)
+    tid = loci["chrom"].astype(np.int64) - 1
+    wins = []
+    ins, dl = t == 1, t == 2
+    wins.append((ins, pos - np.uint64(median), pos + np.uint64(median)))
+    wins.append((dl, pos - np.uint64(wider), pos + np.uint64(narrow)))
+    wins.append((dl, end - np.uint64(narrow), end + np.uint64(narrow)))
+    out = np.empty((n_targets, 2), dtype=np.int64)
+    out[:, 0] = np.iinfo(np.int64).max
+    out[:, 1] = np.iinfo(np.int64).min
+    for sel, s, e in wins:
+        beg = ((s & M) - np.uint64(1)) & M
+        qend = ((e & M) - np.uint64(1)) & M
+        ok = sel & (qend > beg) & (tid >= 0) & (tid < n_targets)
+        if ok.any():
+            np.minimum.at(out[:, 0], tid[ok], beg[ok].astype(np.int64))
+            np.maximum.at(out[:, 1], tid[ok], qend[ok].astype(np.int64))
+    return out
+
+
+def halo_slice(pl: Pileup, loci: np.ndarray, wider: int, median: int, narrow: int) -> Pileup:
+    """The reads any query of `loci` can yield (a rank ingests only its shard's
+    genomic span plus the halo of query windows and read spans).  Keeps per-contig order
+    and tids, so refining `loci` against the slice is bit-identical to the full pileup:
+    every read with pos < q.end and endpos > q.beg for some query q is kept."""
+    span = query_spans(loci, wider, median, narrow, pl.n_targets)
+    keep = np.zeros(pl.n_reads, dtype=bool)
+    tid_off = np.zeros(pl.n_targets + 1, dtype=np.int64)
+    for t in range(pl.n_targets):
+        a, b = int(pl.tid_off[t]), int(pl.tid_off[t + 1])
+        lo, hi = span[t]
+        if b > a and hi > lo:
+            cut = a + int(np.searchsorted(pl.pos[a:b], hi, side="left"))   # pos < hi
+            keep[a:cut] = pl.endpos[a:cut].astype(np.int64) > lo
+        tid_off[t + 1] = tid_off[t] + int(keep[a:b].sum())
+    idx = np.nonzero(keep)[0]
+    starts = pl.cig_off[:-1][idx].astype(np.int64)
+    lens = (pl.cig_off[1:][idx] - pl.cig_off[:-1][idx]).astype(np.int64)
+    cig_off = np.zeros(len(idx) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=cig_off[1:])
+    if len(idx):
+        gather = np.repeat(starts - cig_off[:-1].astype(np.int64), lens) + np.arange(int(cig_off[-1]))
+        cigar = np.ascontiguousarray(pl.cigar[gather])
+    else:
+        cigar = np.zeros(0, dtype=np.uint32)
+    return Pileup(tid_off=tid_off, pos=np.ascontiguousarray(pl.pos[idx]),
+                  endpos=np.ascontiguousarray(pl.endpos[idx]), cig_off=cig_off, cigar=cigar,
+                  clip=None if pl.clip is None else np.ascontiguousarray(pl.clip[idx]),
+                  contig_len=pl.contig_len, flag=None if pl.flag is None else pl.flag[idx])

@@ -1,7 +1,8 @@
 """N>1 plumbing on CPU: world_size 2 (and 3) gloo processes shard the loci and gather the
 results to rank 0 in VCF order.  The per-rank refinement here is the CPU oracle (test
-infrastructure standing in for the GPU, which this container lacks); the sharding,
-padding and gather code is the product's (svtrek_amd.distributed)."""
+infrastructure standing in for the GPU, which this container lacks); the genomic
+sharding, halo slicing, record packing and gather code is the product's
+(svtrek_amd.distributed, svtrek_amd.pileup.halo_slice)."""
 import os
 import socket
 
@@ -9,7 +10,8 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from svtrek_amd.distributed import shard_bounds
+from svtrek_amd.distributed import (PAD_INDEX, genomic_order, pack_records, shard_bounds, shard_rows,
+                                    unpack_records)
 
 
 def _free_port():
@@ -23,13 +25,18 @@ def _worker(rank, world, port, seed, outdir):
 
     import oracle_ffi as O
     from svtrek_amd import sim
-    from svtrek_amd.distributed import run_sharded
+    from svtrek_amd.distributed import gather_results
+    from svtrek_amd.pileup import halo_slice
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     r = sim.generate(sim.SimConfig(seed=seed, n_loci=97, n_targets=2, del_frac=0.6, coverage=12))
-    res = run_sharded(r.loci, lambda l: O.refine_batch(r.pileup, l))
+    rows = shard_rows(r.loci, world, rank)
+    mine = r.loci[rows]
+    sub = halo_slice(r.pileup, mine, 20000, 10000, 2000)
+    assert world == 1 or sub.n_reads < r.pileup.n_reads
+    res = gather_results(rows, O.refine_batch(sub, mine), len(r.loci))
     if rank == 0:
         np.save(os.path.join(outdir, "res.npy"), res.view(np.uint32).reshape(-1, 2))
     dist.barrier()
@@ -56,3 +63,57 @@ def test_shard_bounds_cover_rows_once():
             spans = [shard_bounds(n, world, r) for r in range(world)]
             rows = [i for b0, b1 in spans for i in range(b0, b1)]
             assert rows == list(range(n))
+
+
+def test_genomic_order_is_stable_and_shards_partition():
+    from svtrek_amd.pileup import make_loci
+    loci = make_loci([(2, 2, 500, 900), (2, 1, 700, 900), (1, 1, 700, 0), (2, 2, 100, 900), (2, 1, 700, 800)])
+    assert genomic_order(loci).tolist() == [1, 2, 4, 3, 0]
+    for world in (1, 2, 3, 8):
+        got = np.concatenate([shard_rows(loci, world, r) for r in range(world)])
+        assert got.tolist() == [1, 2, 4, 3, 0]
+
+
+def test_pack_unpack_records_roundtrip():
+    from svtrek_amd._lib import RESULT_DTYPE
+    rng = np.random.default_rng(3)
+    n, world = 23, 4
+    res = np.zeros(n, dtype=RESULT_DTYPE)
+    res["start"] = rng.integers(0, 2**32, n, dtype=np.uint64)
+    res["end"] = rng.integers(0, 2**32, n, dtype=np.uint64)
+    perm = rng.permutation(n)
+    per = (n + world - 1) // world
+    bufs = [pack_records(perm[b0:b1], res[perm[b0:b1]], per)
+            for b0, b1 in (shard_bounds(n, world, r) for r in range(world))]
+    assert all(b.shape == (per, 4) for b in bufs)
+    assert (bufs[-1][n - per * (world - 1):, 0] == PAD_INDEX).all()
+    back = unpack_records(np.concatenate(bufs), n)
+    np.testing.assert_array_equal(back.view(np.uint32), res.view(np.uint32))
+    with pytest.raises(RuntimeError):
+        unpack_records(np.concatenate(bufs[:-1]), n)
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_halo_slice_is_exact(seed):
+    """Refining a shard against its halo slice equals refining it against the whole pileup,
+    including wrapped windows near the contig start, INS/INV loci, unknown contigs and
+    non-default intervals."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
+    import oracle_ffi as O
+    from svtrek_amd import Params, sim
+    from svtrek_amd.pileup import halo_slice, make_loci
+    r = sim.generate(sim.SimConfig(seed=seed, n_loci=160, n_targets=3, del_frac=0.5, coverage=10))
+    extra = make_loci([(2, 1, 30, 400), (1, 1, 5, 0), (3, 1, 100, 9000), (2, 9, 5000, 9000),
+                       (2, 0, 5000, 9000), (2, 2, 0xFFFFFF00, 0xFFFFFFF0)])
+    loci = np.concatenate([r.loci, extra])
+    for prm in (Params(), Params(wider_interval=3000, median_interval=700, narrow_interval=300)):
+        full = O.refine_batch(r.pileup, loci, prm)
+        for world in (2, 5):
+            for rank in range(world):
+                rows = shard_rows(loci, world, rank)
+                sub = halo_slice(r.pileup, loci[rows], prm.wider_interval, prm.median_interval,
+                                 prm.narrow_interval)
+                got = O.refine_batch(sub, loci[rows], prm)
+                np.testing.assert_array_equal(got.view(np.uint32), full[rows].view(np.uint32))

@@ -103,3 +103,22 @@ def test_audt_dist_single_rank(tmp_path):
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600, cwd=ROOT, env=env)
     assert res.returncode == 0, res.stderr[-2000:]
     assert res.stdout == O.audit_text(vcf.read_text(), r.pileup)
+
+
+def test_genomic_shards_on_one_device(tmp_path):
+    """--devices 0,0,0: three genomic shards, each with its own halo-sliced pileup and its own
+    context on GPU 0, print the same bytes as one shard (SURVEY §8(e) partitioning)."""
+    r = sim.generate(sim.SimConfig(seed=61, n_targets=3, n_loci=240, del_frac=0.5, coverage=15), keep_handle=True)
+    bam = str(tmp_path / "s.bam")
+    sim.write_bam(r, bam)
+    vcf = tmp_path / "s.vcf"
+    sim.write_vcf(r.loci, str(vcf))
+    lines = vcf.read_text().splitlines(keepends=True)
+    head = [l for l in lines if l.startswith("#")]
+    body = [l for l in lines if not l.startswith("#")]
+    random.Random(5).shuffle(body)                     # VCF order != genomic order
+    text = "".join(head + body)
+    vcf.write_text(text)
+    want = O.audit_text(text, r.pileup)
+    assert run_cli("-b", bam, "-v", str(vcf), "--devices", "0,0,0", "--batch", "50").stdout == want
+    assert run_cli("-b", bam, "-v", str(vcf), "--devices", "0,0").stdout == want
