@@ -138,6 +138,26 @@ svt_status svt_sync(svt_ctx *ctx, void *hip_stream);
 /* Count the reference algorithm's work for n host loci (diagnostic, synchronous). */
 svt_status svt_count_work(svt_ctx *ctx, const svt_locus *loci, size_t n, svt_work *out);
 
+/* ---- optional mode: sliding_window_ins (reference sliding_window.c:8-97) ------------
+ * Replaces int sliding_window_ins(int chrom, interval inter, t_arg *params, int
+ * windowSize, int slideSize) (sliding_window.c:8; declared as refine_ins_disc in
+ * sliding_window.h:11; the reference never calls it).  Query i covers the sub-windows
+ * [s, min(s + window_size, end)) for s = start, start + window_size, ... < end; each is
+ * refine_ins's region query and CIGAR walk, voted by sliding support (consensus_min_count
+ * of the context's params).  best[i] = bestCandidateOverall (-1 = none).  If `sub` is not
+ * NULL it receives, for every sub-window in query order, {bestCandidate, maxSupport}; the
+ * reference prints "INS Discovery in window [%d, %d] at position %d with support %d\n"
+ * for each sub-window whose bestCandidate != -1.  Synchronous.
+ * EINVAL: window_size < 1 or slide_size < 1 (the reference loops forever), or
+ * end + window_size > 2^32 (its uint32 sub_start wraps). */
+typedef struct svt_sw_query { int32_t chrom; uint32_t start, end; } svt_sw_query;
+typedef struct svt_sw_window { int32_t candidate, support; } svt_sw_window;
+
+/* Sub-windows of one query: ceil((end - start) / window_size), 0 when end <= start. */
+uint64_t   svt_sw_subwindows(const svt_sw_query *q, int32_t window_size);
+svt_status svt_sliding_window_ins(svt_ctx *ctx, const svt_sw_query *q, size_t n, int32_t window_size,
+                                  int32_t slide_size, int32_t *best, svt_sw_window *sub);
+
 /* Bytes of device memory the loaded pileup occupies. */
 uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
 

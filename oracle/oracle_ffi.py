@@ -57,6 +57,8 @@ def lib() -> C.CDLL:
         L.orc_audit_text.argtypes = [C.c_char_p, C.c_size_t, P, P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
         L.orc_audit_text.restype = C.c_int
         L.orc_free.argtypes = [P]
+        L.orc_sliding_window_ins.argtypes = [P, C.c_int, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, P, P]
+        L.orc_sliding_window_ins.restype = C.c_int
         _lib = L
     return _lib
 
@@ -122,3 +124,17 @@ def audit_text(vcf_text: str, pl, prm=None) -> str:
     lib().orc_free(out)
     del keep
     return s
+
+
+def sliding_window_ins(pl, chrom: int, start: int, end: int, window_size: int, slide_size: int,
+                       min_count: int = 3):
+    """-> (bestCandidateOverall, int32 candidate per sub-window, int32 support per sub-window)"""
+    v, keep = pileup(pl)
+    ws = max(int(window_size), 1)
+    nsub = max(0, (int(end) - int(start) + ws - 1) // ws)
+    cand = np.empty(nsub, dtype=np.int32)
+    sup = np.empty(nsub, dtype=np.int32)
+    best = lib().orc_sliding_window_ins(C.byref(v), chrom, start & 0xFFFFFFFF, end & 0xFFFFFFFF, window_size,
+                                        slide_size, min_count, cand.ctypes.data, sup.ctypes.data)
+    del keep
+    return best, cand, sup

@@ -60,6 +60,14 @@ void orc_refine_locus(const orc_pileup *p, const orc_params *prm, const orc_locu
 int  orc_refine_batch(const orc_pileup *p, const orc_params *prm, const orc_locus *loci,
                       size_t n, orc_result *out, int threads, orc_work *w);
 
+/* sliding_window_ins (sliding_window.c:8-97; dead code in the reference -- no caller).
+ * Sub-windows [s, min(s+ws, end)) for s = start, start+ws, ... < end; per sub-window the
+ * INS walk of refine_ins and a sliding-support vote.  sub_cand/sub_support (may be NULL)
+ * receive each sub-window's bestCandidate (-1: none / no line printed) and maxSupport;
+ * returns bestCandidateOverall.  Requires ws >= 1, slide >= 1, end + ws <= 2^32. */
+int orc_sliding_window_ins(const orc_pileup *p, int chrom, uint32_t start, uint32_t end, int window_size,
+                           int slide_size, int min_count, int32_t *sub_cand, int32_t *sub_support);
+
 /* A1: parse one VCF data line (modified in place, as strtok_r does).  Returns
  * 1 = record reaches the type switch (*l filled), 0 = skipped silently,
  * 2 = skipped with a stderr message (text copied into err). */

@@ -26,6 +26,8 @@ SVT_LDS_CANDS = 256
 
 LOCUS_DTYPE = np.dtype([("type", "<i4"), ("chrom", "<i4"), ("pos", "<u4"), ("end", "<u4")])
 RESULT_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4")])
+SW_QUERY_DTYPE = np.dtype([("chrom", "<i4"), ("start", "<u4"), ("end", "<u4")])     # svt_sw_query
+SW_WINDOW_DTYPE = np.dtype([("candidate", "<i4"), ("support", "<i4")])               # svt_sw_window
 
 
 class SvtParams(C.Structure):
@@ -66,6 +68,7 @@ class SvtWork(C.Structure):
 ENGINE_SYMBOLS = (
     "svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
     "svt_count_work", "svt_pileup_device_bytes", "svt_last_error", "svt_close", "svt_version",
+    "svt_sw_subwindows", "svt_sliding_window_ins",
 )
 
 _engine = None
@@ -99,8 +102,11 @@ def load_engine() -> C.CDLL:
     lib.svt_close.argtypes = [P]
     lib.svt_close.restype = None
     lib.svt_version.restype = C.c_char_p
+    lib.svt_sw_subwindows.argtypes = [P, C.c_int32]
+    lib.svt_sw_subwindows.restype = C.c_uint64
+    lib.svt_sliding_window_ins.argtypes = [P, P, C.c_size_t, C.c_int32, C.c_int32, P, P]
     for name in ("svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
-                 "svt_count_work"):
+                 "svt_count_work", "svt_sliding_window_ins"):
         getattr(lib, name).restype = C.c_int32
     _engine = lib
     return lib

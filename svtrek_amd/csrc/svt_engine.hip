@@ -65,6 +65,7 @@ struct DevPileup {
 
 struct KParams {
     int32_t wider, median, narrow, range, ci, min_count;
+    int32_t sw_window, sw_slide;   // sliding_window_ins mode only
 };
 
 struct KArgs {
@@ -78,6 +79,8 @@ struct KArgs {
     unsigned long long pool_words;
     int32_t *status;            // bit0: spill pool exhausted
     unsigned long long *work;   // svt_work counters (COUNT builds only)
+    const uint4 *sw_sub;        // sliding_window_ins mode: per sub-window {chrom, start, end, 0}
+    int2 *sw_out;               //   per sub-window {bestCandidate, maxSupport}
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -611,8 +614,45 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
     return distL < distR ? valL : valR;   // refinement.c:100
 }
 
+// sliding_window_ins's vote (sliding_window.c:65-84) on sorted A[0..n) with prefix sums
+// P[0..n]: for i = 0, slide, 2*slide, ...: support = #{j >= i : A[j] - A[i] <= ws}; the
+// first i reaching the largest support >= min_count wins, its candidate is the rounded
+// mean of A[i..i+support) in the reference's 32-bit int arithmetic (sum wraps mod 2^32).
+__device__ __forceinline__ int32_t sw_vote(const int32_t *A, const int64_t *P, int32_t n, const KParams &k,
+                                           int32_t &support_out) {
+    const int ln = lane_id();
+    const int32_t ws = k.sw_window, slide = k.sw_slide;
+    const int32_t nstart = (n + slide - 1) / slide;
+    int32_t best_sup = 0, best_i = -1;
+    for (int32_t b = 0; b < nstart; b += WAVE) {
+        const int32_t t = b + ln;
+        int32_t sup = 0, i = 0;
+        if (t < nstart) {
+            i = t * slide;
+            sup = first_greater(A, i, n, (int64_t)A[i] + ws) - i;         // :71-75
+        }
+        const bool ok = sup >= k.min_count;                                  // :76
+        // wave max of qualifying supports; ties -> the smallest i (strict > in :76)
+        int32_t m = wave_scan_max(ok ? sup : -1);
+        m = rdlane_i(m, WAVE - 1);
+        if (m > best_sup) {
+            const uint64_t at = ballot(ok && sup == m);
+            best_sup = m;
+            best_i = rdlane_i(i, __builtin_ctzll(at));
+        }
+    }
+    support_out = best_sup;
+    if (best_i < 0) return -1;
+    const uint32_t sum = (uint32_t)(uint64_t)(P[best_i + best_sup] - P[best_i]);      // :78-81, int wrap
+    return (int32_t)(sum + (uint32_t)(best_sup / 2)) / best_sup;                      // :82
+}
+
+constexpr int V_CONSENSUS = 0, V_SLIDING = 1;
+
 // Sort + prefix sums + vote over buf[0..n) with scratch for P (n+1 int64).
-__device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k) {
+template <int VOTE>
+__device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
+                                                 int32_t &support) {
     const int ln = lane_id();
     int N = 1;
     while (N < n) N <<= 1;
@@ -629,6 +669,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
         carry = (int64_t)rdlane64((uint64_t)s, WAVE - 1);
     }
     wave_sync();
+    if (VOTE == V_SLIDING) return sw_vote(buf, P, n, k, support);
     return vote(buf, P, n, pos, k);
 }
 
@@ -652,17 +693,18 @@ __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, u
     return uniform_i(*sink.cnt);
 }
 
-template <int KIND, bool COUNT, bool STREAM>
+template <int KIND, bool COUNT, bool STREAM, int VOTE = V_CONSENSUS>
 __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e, uint32_t imprecise,
-                                 unsigned long long *wk) {
+                                 unsigned long long *wk, int32_t &support) {
     WinStats st;
     Sink sink{lds.cand, CAP, &lds.ncand};
     int32_t n = gather<KIND, COUNT, STREAM>(a, chrom - 1, s, e, sink, st, lds.sl);
     if (COUNT && lane_id() == 0) {
         wk[0] += 1; wk[1] += st.reads; wk[2] += st.ops; wk[3] += (unsigned long long)n;
     }
-    if (n < a.prm.min_count) return -1;                    // refinement.c:43-45
-    if (n <= CAP) return sort_and_vote(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm);
+    support = 0;
+    if (n < a.prm.min_count) return -1;                    // refinement.c:43-45 (sliding: no support >= min_count)
+    if (n <= CAP) return sort_and_vote<VOTE>(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm, support);
     // spill: a slab for N ints + (n+1) int64 from the device pool, then re-gather into it
     if (COUNT && lane_id() == 0) wk[4] += 1;
     int N = 1;
@@ -680,7 +722,7 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     WinStats st2;
     Sink s2{g, N, &lds.ncand};
     gather<KIND, false, STREAM>(a, chrom - 1, s, e, s2, st2, lds.sl);
-    return sort_and_vote(g, gp, n, (int32_t)imprecise, a.prm);
+    return sort_and_vote<VOTE>(g, gp, n, (int32_t)imprecise, a.prm, support);
 }
 
 // One wave per query window, WPB independent waves per workgroup.  Window g < n is locus
@@ -717,19 +759,20 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_kernel(KArgs a) {
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
     unsigned long long wk[5] = {0, 0, 0, 0, 0};
     uint32_t r = SVT_NA;
+    int32_t sup;
     const KParams &k = a.prm;
     if (type == T_INS) {                                   // audit.c:176-187
         if (w == 0) {
             uint32_t s = pos - (uint32_t)k.median, e = pos + (uint32_t)k.median;
-            r = (uint32_t)refine_window<K_INS, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk);
+            r = (uint32_t)refine_window<K_INS, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk, sup);
         }
     } else if (type == T_DEL) {                            // audit.c:188-220
         if (w == 0) {
             uint32_t s = pos - (uint32_t)k.wider, e = pos + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_START, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk);
+            r = (uint32_t)refine_window<K_START, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk, sup);
         } else {
             uint32_t s = end - (uint32_t)k.narrow, e = end + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_END, COUNT, STREAM>(a, lds, chrom, s, e, end, wk);
+            r = (uint32_t)refine_window<K_END, COUNT, STREAM>(a, lds, chrom, s, e, end, wk, sup);
         }
     }
     // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250), so both
@@ -741,6 +784,36 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_kernel(KArgs a) {
             for (int i = 0; i < 5; i++)
                 if (wk[i]) atomicAdd(a.work + i, wk[i]);
     }
+}
+
+// sliding_window_ins mode (sliding_window.c:8-97): one wave per sub-window.  A sub-window
+// is refine_ins's window exactly -- the same region query (sub_start-1, sub_end-1, :27),
+// the same walk (I >= 50 collects rp, advance unless I/S, break when rp > sub_end,
+// :30-54) -- so it reuses the stream gather; only the vote differs (sw_vote).
+__global__ __launch_bounds__(64 * WPB) void sw_kernel(KArgs a) {
+    __shared__ WinLds lds_all[WPB];
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x * WPB + wid;
+    if (g >= a.n) return;
+    const uint4 q = a.sw_sub[g];
+    const int32_t chrom = uniform_i((int32_t)q.x);
+    const uint32_t s = (uint32_t)uniform_i((int32_t)q.y), e = (uint32_t)uniform_i((int32_t)q.z);
+    unsigned long long wk[5];
+    int32_t sup = 0;
+    const int32_t c = refine_window<K_INS, false, true, V_SLIDING>(a, lds_all[wid], chrom, s, e, 0u, wk, sup);
+    if (lane_id() == 0) a.sw_out[g] = make_int2(c, sup);
+}
+
+// bestCandidateOverall per query over its sub-windows in order (sliding_window.c:86-92).
+__global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t nq, int32_t *best) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    int32_t b = -1, m = 0;
+    for (uint64_t k = off[q]; k < off[q + 1]; k++) {
+        const int2 v = sub[k];
+        if (v.x != -1 && v.y > m) { m = v.y; b = v.x; }
+    }
+    best[q] = b;
 }
 
 }  // namespace
@@ -803,7 +876,7 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
                        c->d_maxspan, c->d_cigar, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
-                    c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count};
+                    c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
     a.loci = d_loci;
     a.out = d_out;
     a.n = n;
@@ -812,6 +885,8 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
     a.pool_words = c->pool_words;
     a.status = (int32_t *)(c->d_ctl + 8);
     a.work = count ? (unsigned long long *)(c->d_ctl + 16) : nullptr;
+    a.sw_sub = nullptr;
+    a.sw_out = nullptr;
     return a;
 }
 
@@ -1036,6 +1111,76 @@ svt_status svt_count_work(svt_ctx *c, const svt_locus *loci, size_t n, svt_work 
     out->windows = w[0]; out->reads = w[1]; out->ops_walked = w[2]; out->candidates = w[3];
     out->spilled_windows = w[4];
     return SVT_OK;
+}
+
+uint64_t svt_sw_subwindows(const svt_sw_query *q, int32_t window_size) {
+    if (!q || window_size < 1 || q->end <= q->start) return 0;
+    return ((uint64_t)(q->end - q->start) + (uint64_t)window_size - 1) / (uint64_t)window_size;
+}
+
+svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, int32_t window_size,
+                                  int32_t slide_size, int32_t *best, svt_sw_window *sub) {
+    if (!c) return SVT_EINVAL;
+    if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
+    if (window_size < 1 || slide_size < 1)
+        return fail(c, SVT_EINVAL, "%s", "window_size and slide_size must be >= 1 (the reference loops forever)");
+    if (n == 0) return SVT_OK;
+    if (!q || !best) return fail(c, SVT_EINVAL, "%s", "null queries/best");
+    std::vector<uint64_t> off(n + 1, 0);
+    for (size_t i = 0; i < n; i++) {
+        if ((uint64_t)q[i].end + (uint64_t)window_size > 0x100000000ull)
+            return fail(c, SVT_EINVAL, "%s", "end + window_size > 2^32 (sub_start wraps, sliding_window.c:12)");
+        off[i + 1] = off[i] + svt_sw_subwindows(q + i, window_size);
+    }
+    const uint64_t ns = off[n];
+    if (ns > 0x3fffffffull) return fail(c, SVT_EINVAL, "%s", "more than 2^30-1 sub-windows in one call");
+    std::vector<uint4> subs((size_t)ns);
+    for (size_t i = 0; i < n; i++) {
+        uint64_t k = off[i];
+        for (uint32_t ss = q[i].start; ss < q[i].end; ss += (uint32_t)window_size, k++) {   // :12-15
+            uint32_t se = ss + (uint32_t)window_size;
+            subs[(size_t)k] = make_uint4((uint32_t)q[i].chrom, ss, se > q[i].end ? q[i].end : se, 0u);
+        }
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    uint4 *d_sub = nullptr;
+    int2 *d_res = nullptr;
+    uint64_t *d_off = nullptr;
+    int32_t *d_best = nullptr;
+    svt_status s = SVT_OK;
+    auto cleanup = [&]() { hfree(d_sub); hfree(d_res); hfree(d_off); hfree(d_best); };
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && s == SVT_OK) s = fail(c, SVT_EDEVICE, what, hipGetErrorString(e));
+        return s == SVT_OK;
+    };
+    if (chk(hipMalloc(&d_sub, std::max<size_t>(1, (size_t)ns) * sizeof(uint4)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_res, std::max<size_t>(1, (size_t)ns) * sizeof(int2)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_off, (n + 1) * sizeof(uint64_t)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_best, n * sizeof(int32_t)), "hipMalloc: %s") &&
+        (ns == 0 || chk(hipMemcpy(d_sub, subs.data(), (size_t)ns * sizeof(uint4), hipMemcpyHostToDevice), "H2D: %s")) &&
+        chk(hipMemcpy(d_off, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice), "H2D: %s") &&
+        chk(hipMemsetAsync(c->d_ctl, 0, 64, nullptr), "hipMemset: %s")) {
+        if (ns) {
+            KArgs a = make_args(c, nullptr, nullptr, (uint32_t)ns, false);
+            a.prm.sw_window = window_size;
+            a.prm.sw_slide = slide_size;
+            a.sw_sub = d_sub;
+            a.sw_out = d_res;
+            hipLaunchKernelGGL(sw_kernel, dim3((unsigned)((ns + WPB - 1) / WPB)), dim3(64 * WPB), 0, nullptr, a);
+            chk(hipGetLastError(), "sw_kernel: %s");
+        }
+        if (s == SVT_OK) {
+            hipLaunchKernelGGL(sw_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, d_res,
+                               d_off, (uint32_t)n, d_best);
+            chk(hipGetLastError(), "sw_reduce_kernel: %s");
+        }
+        if (s == SVT_OK) s = svt_sync(c, nullptr);
+        if (s == SVT_OK) chk(hipMemcpy(best, d_best, n * sizeof(int32_t), hipMemcpyDeviceToHost), "D2H: %s");
+        if (s == SVT_OK && sub && ns)
+            chk(hipMemcpy(sub, d_res, (size_t)ns * sizeof(int2), hipMemcpyDeviceToHost), "D2H: %s");
+    }
+    cleanup();
+    return s;
 }
 
 uint64_t svt_pileup_device_bytes(const svt_ctx *c) { return c ? c->dev_bytes : 0; }

@@ -13,7 +13,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (LOCUS_DTYPE, RESULT_DTYPE, STATUS_NAMES, SvtParams, SvtWork, load_engine, ptr)
+from ._lib import (LOCUS_DTYPE, RESULT_DTYPE, STATUS_NAMES, SW_QUERY_DTYPE, SW_WINDOW_DTYPE, SvtParams, SvtWork,
+                   load_engine, ptr)
 from .pileup import Pileup
 
 # params.h:27-32
@@ -90,6 +91,26 @@ class Engine:
         w = SvtWork()
         self._check(self.lib.svt_count_work(self._h, ptr(loci), len(loci), C.byref(w)))
         return {f: int(getattr(w, f)) for f, _ in SvtWork._fields_}
+
+    def sliding_window_ins(self, queries: np.ndarray, window_size: int, slide_size: int,
+                           with_subwindows: bool = False):
+        """sliding_window_ins (reference sliding_window.c:8-97) for every query
+        {chrom, start, end} (SW_QUERY_DTYPE): int32 bestCandidateOverall per query (-1 = none),
+        plus, with `with_subwindows`, (offsets, SW_WINDOW_DTYPE per sub-window in order).
+        Uses this engine's consensus_min_count."""
+        q = np.ascontiguousarray(queries, dtype=SW_QUERY_DTYPE)
+        best = np.empty(len(q), dtype=np.int32)
+        sub = None
+        off = None
+        if with_subwindows:
+            off = np.zeros(len(q) + 1, dtype=np.int64)
+            ws = max(int(window_size), 1)
+            span = q["end"].astype(np.int64) - q["start"].astype(np.int64)
+            off[1:] = np.cumsum(np.where(span > 0, (span + ws - 1) // ws, 0))
+            sub = np.empty(int(off[-1]), dtype=SW_WINDOW_DTYPE)
+        self._check(self.lib.svt_sliding_window_ins(self._h, ptr(q), len(q), int(window_size), int(slide_size),
+                                                    ptr(best), ptr(sub)))
+        return (best, off, sub) if with_subwindows else best
 
     @property
     def device_bytes(self) -> int:

@@ -96,3 +96,19 @@ def format_result(locus: np.void, result: np.void) -> str:
     buf = C.create_string_buffer(512)
     n = L.svth_format(lo.ctypes.data, r.ctypes.data, buf, 512)
     return buf.raw[:n].decode("latin-1")
+
+
+def format_sw_lines(queries: np.ndarray, off: np.ndarray, sub: np.ndarray, window_size: int) -> str:
+    """The stdout lines sliding_window_ins prints (sliding_window.c:86-87) for the
+    sub-windows of `queries`, in order: one per sub-window whose bestCandidate != -1."""
+    out = []
+    for i, q in enumerate(queries):
+        s0, e0 = int(q["start"]), int(q["end"])
+        for k in range(int(off[i]), int(off[i + 1])):
+            ss = (s0 + (k - int(off[i])) * window_size) & 0xFFFFFFFF
+            se = min(ss + window_size, e0)
+            c, sp = int(sub[k]["candidate"]), int(sub[k]["support"])
+            if c != -1:
+                i32 = lambda x: x - (1 << 32) if x >= (1 << 31) else x   # noqa: E731  (%d of uint32)
+                out.append(f"INS Discovery in window [{i32(ss)}, {i32(se)}] at position {c} with support {sp}\n")
+    return "".join(out)
