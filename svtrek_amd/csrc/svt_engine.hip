@@ -35,7 +35,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.4.1 (gfx950, window-stream kernel)"
+#define SVT_VERSION "svtrek_amd 0.5.0 (gfx950, window-stream kernel)"
 
 namespace {
 
@@ -816,6 +816,30 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
     best[q] = b;
 }
 
+// svt_load_pileup's per-op work, on the device: one wave per read copies the read's
+// CIGAR words from the caller's unpadded layout into the padded arena (coalesced) and
+// sums the reference advance (refinement.c:141) to flag reads whose walk reaches 2^31
+// (SLOW_BIT: those take walk_read's exact uint32 replay).  The host only does per-read
+// work (offsets, prefix-max, buckets).
+__global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ raw, const uint64_t *__restrict__ raw_off,
+                                                   const uint64_t *__restrict__ poff, uint4 *rec,
+                                                   uint32_t *__restrict__ arena, int64_t nr) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nr) return;
+    const int ln = lane_id();
+    const uint64_t o0 = raw_off[r], n = raw_off[r + 1] - o0, dst = poff[r];
+    uint64_t walk = 0;
+    for (uint64_t i = (uint64_t)ln; i < n; i += WAVE) {
+        const uint32_t w = raw[o0 + i];
+        arena[dst + i] = w;
+        const uint32_t op = w & 0xfu;
+        if (op != OP_INS && op != OP_SOFT) walk += w >> 4;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) walk += __shfl_xor(walk, d, WAVE);
+    if (ln == 0 && (uint64_t)rec[r].x + walk >= (1ull << 31)) rec[r].z |= SLOW_BIT;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1005,20 +1029,13 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
             if (p->clip) clip = p->clip[r] & 3u;
             else clip = ncig ? (((p->cigar[o1 - 1] & 0xfu) == OP_SOFT ? 1u : 0u) |
                                 ((p->cigar[o0] & 0xfu) == OP_SOFT ? 2u : 0u)) : 0u;
-            // the stream kernel needs every walk position (from pos, or from a dead read's
-            // inter.end+1 start) to stay below 2^32; reads walking >= 2^31 take the exact slow walk
-            uint64_t walk = (uint64_t)(uint32_t)p->pos[r];
-            for (uint64_t i = o0; i < o1; i++) {
-                uint32_t op = p->cigar[i] & 0xfu;
-                if (op != OP_INS && op != OP_SOFT) walk += p->cigar[i] >> 4;
-            }
-            const uint32_t slow = walk >= (1ull << 31) ? SLOW_BIT : 0u;
+            // SLOW_BIT (walk >= 2^31) is set by pack_kernel on the device
             if (p->endpos[r] > m) m = p->endpos[r];
             if (p->endpos[r] - p->pos[r] > ms) ms = p->endpos[r] - p->pos[r];
             maxpos = std::max(maxpos, p->pos[r]);
             emax[(size_t)r] = m;
             poff[(size_t)r] = pw;
-            rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | slow | (clip << 30),
+            rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | (clip << 30),
                                         (uint32_t)pw);
             pw += ((uint64_t)ncig + (OPL - 1)) & ~(uint64_t)(OPL - 1);
         }
@@ -1036,12 +1053,6 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     }
     poff[(size_t)nr] = pw;
     bkt_off[(size_t)nt] = (int64_t)bkt.size();
-    // padded arena: read r's ops at poff[r], zero words (0M) up to the next multiple of OPL
-    std::vector<uint32_t> arena((size_t)pw + CIGAR_PAD, 0u);
-    for (int64_t r = 0; r < nr; r++) {
-        uint64_t o0 = p->cig_off[r], n = p->cig_off[r + 1] - o0;
-        if (n) memcpy(arena.data() + poff[(size_t)r], p->cigar + o0, n * 4);
-    }
     svt_status s;
     if ((s = upload(c, c->d_pos, p->pos, (size_t)nr))) return s;
     if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
@@ -1052,7 +1063,26 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
     if (nt > 0) { if ((s = upload(c, c->d_tid_off, p->tid_off, (size_t)nt + 1))) return s; }
     else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
-    if ((s = upload(c, c->d_cigar, arena.data(), arena.size()))) return s;
+    // padded arena: read r's ops at poff[r], zero words (0M) up to the next multiple of OPL,
+    // then CIGAR_PAD zero words; filled on the device from the caller's unpadded words
+    if ((s = upload<uint32_t>(c, c->d_cigar, nullptr, 0, (size_t)pw + CIGAR_PAD))) return s;
+    if (nr > 0) {
+        uint32_t *d_raw = nullptr;
+        uint64_t *d_raw_off = nullptr;
+        hipError_t e = hipMalloc(&d_raw, std::max<uint64_t>(nops, 1) * 4);
+        if (e == hipSuccess) e = hipMalloc(&d_raw_off, ((size_t)nr + 1) * 8);
+        if (e == hipSuccess && nops) e = hipMemcpy(d_raw, p->cigar, nops * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, d_raw, d_raw_off,
+                               c->d_off64, c->d_rec, c->d_cigar, (int64_t)nr);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        hfree(d_raw);
+        hfree(d_raw_off);
+        if (e != hipSuccess) return fail(c, SVT_EDEVICE, "pileup pack: %s", hipGetErrorString(e));
+    }
     c->n_targets = nt;
     c->n_reads = nr;
     c->n_ops = nops;

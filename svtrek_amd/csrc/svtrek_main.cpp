@@ -265,6 +265,7 @@ int audit(int argc, char **argv) {
     const int G = a.gpus;
     std::vector<int> rc(G, 0);
     std::vector<std::string> gerr(G);
+    std::vector<double> load_s(G, 0.0);
     std::vector<size_t> order;
     if (G > 1) {
         order.resize(loci.size());
@@ -281,6 +282,7 @@ int audit(int argc, char **argv) {
         svt_result *out = res.data();
         size_t n = loci.size();
         Shard sh;
+        const double tl = now_s();
         if (G > 1) {
             size_t per = (n + G - 1) / G, b0 = std::min(n, per * (size_t)g), b1 = std::min(n, b0 + per);
             build_shard(view, loci, std::vector<size_t>(order.begin() + b0, order.begin() + b1), a.prm, sh);
@@ -291,6 +293,7 @@ int audit(int argc, char **argv) {
         } else {
             s = svt_load_pileup(ctx, &view);
         }
+        load_s[g] = now_s() - tl;
         for (size_t k = 0; !s && k < n; k += a.batch) {
             size_t m = std::min(a.batch, n - k);
             s = svt_refine_batch(ctx, in + k, m, out + k);
@@ -322,8 +325,9 @@ int audit(int argc, char **argv) {
     fwrite(out.data(), 1, out.size(), stdout);
     printf("[INFO] Ended processing variation file\n");
     if (a.verbose)   // --verbose is parsed but unused by the reference; here: stage timings on stderr
-        fprintf(stderr, "[svtrek_amd] ingest %.3fs  vcf-parse %.3fs  load+refine %.3fs  print %.3fs  records %zu\n",
-                t_ingest - t0, t_parse - t_ingest, t_refine - t_parse, now_s() - t_refine, loci.size());
+        fprintf(stderr, "[svtrek_amd] ingest %.3fs  vcf-parse %.3fs  load+refine %.3fs (load %.3fs)  print %.3fs  records %zu\n",
+                t_ingest - t0, t_parse - t_ingest, t_refine - t_parse, *std::max_element(load_s.begin(), load_s.end()),
+                now_s() - t_refine, loci.size());
     return 0;
 }
 

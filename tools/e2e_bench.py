@@ -42,20 +42,21 @@ def main() -> int:
     times = []
     for _ in range(a.reps):
         t = time.perf_counter()
-        p = subprocess.run([cli, "audt", "-b", bam, "-v", vcf, "-t", str(a.t)], stdout=subprocess.PIPE,
+        p = subprocess.run([cli, "audt", "-b", bam, "-v", vcf, "-t", str(a.t), "--verbose"], stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE, timeout=1800)
         times.append(time.perf_counter() - t)
         if p.returncode != 0:
             print(p.stderr.decode()[-2000:], file=sys.stderr)
             return p.returncode
     lines = p.stdout.count(b"\n") - 2
+    stages = [l for l in p.stderr.decode(errors="replace").splitlines() if l.startswith("[svtrek_amd]")]
     best = min(times)
     print(json.dumps({
         "metric": "end-to-end svtrek audt (BAM ingest + H2D + refine + print)", "workload": a.workload,
         "loci": int(len(r.loci)), "printed_records": int(lines), "bam_bytes": os.path.getsize(bam),
         "with_seq": a.with_seq, "inflate_threads": a.t, "seconds_best": round(best, 3),
         "seconds_all": [round(x, 3) for x in times], "loci_per_s": round(len(r.loci) / best, 1),
-        "prep_seconds": round(prep, 1)}))
+        "prep_seconds": round(prep, 1), "stages_last_run": stages[-1] if stages else None}))
     return 0
 
 
