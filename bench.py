@@ -75,6 +75,11 @@ def cpu_baseline(res, n_threads: int, budget_s: float = 20.0) -> dict:
     }
 
 
+def _engine_version() -> str:
+    from svtrek_amd import version
+    return version()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,7 +182,7 @@ def main() -> int:
     # were taken on this engine version and workload (tools/gpu_profile.sh -> profiles/traffic.json)
     traffic = traffic_src = None
     try:
-        from svtrek_amd import version as _ver
+        _ver = _engine_version
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
         if tj.get("engine_version") == _ver() and tj.get("workload") == args.workload:
@@ -222,6 +227,7 @@ def main() -> int:
             "work": work,
             "setup_s": {"generate": round(gen_s, 2), "load_pileup": round(load_s, 2)},
             "pileup_device_bytes": eng.device_bytes,
+            "engine_version": _engine_version(),
         }
         print(json.dumps(out), flush=True)
     eng.close()
