@@ -15,7 +15,8 @@ run() {  # name, timeout, cmd...
   echo "[$(date +%T)] end $name rc=$rc" >> "$OUT/steps.log"
   return $rc
 }
-run pytest 600 python -m pytest tests -m gpu -x -q; rc=$?
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+run pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread; rc=$?
 tail -5 "$OUT/pytest.log"
 if [ $rc -gt 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
 run bench_stream 300 python bench.py --steps 20 --warmup 3 || exit $?
