@@ -35,7 +35,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.5.0 (gfx950, window-stream kernel)"
+#define SVT_VERSION "svtrek_amd 0.6.0 (gfx950, chunk-index walk)"
 
 namespace {
 
@@ -49,6 +49,17 @@ constexpr int BKT_SHIFT = 12;               // read-start bucket = 4096 bp
 constexpr uint32_t NCIG_MASK = 0x1fffffffu; // rec.z: n_cigar | slow << 29 | clip << 30
 constexpr uint32_t SLOW_BIT = 1u << 29;
 constexpr uint32_t CIGAR_PAD = 1040;        // zero words after the arena (tile over-read)
+// Arena alignment: every read's CIGAR starts on a multiple of ALIGN_OPS words (zero-word
+// padding = 0M ops: advance nothing, never a candidate).  The chunk index holds one word
+// per CHUNK ops of the padded arena.
+constexpr int CHUNK = 8;                    // ops per chunk
+constexpr int CPL = 4;                      // chunks per lane in the index walk
+constexpr int ALIGN_OPS = CHUNK * CPL;      // 32 ops: a lane's chunks belong to one read
+constexpr uint32_t CH_POS = 0x3fffffffu;    // chunk word: walk position after the chunk's last op
+constexpr uint32_t CH_DEL = 1u << 30;       //   the chunk holds a D op with len > 50  (refinement.c:124,:190)
+constexpr uint32_t CH_INS = 1u << 31;       //   the chunk holds an I op with len >= 50 (refinement.c:299)
+constexpr uint32_t CHUNK_PAD = 272;         // zero words after the chunk index (tile over-read)
+constexpr uint64_t INDEX_LIMIT = 1ull << 30; // walks reaching 2^30 are flagged slow (chunk word has 30 bits)
 
 struct DevPileup {
     const int32_t *pos;       // [n_reads]
@@ -60,6 +71,7 @@ struct DevPileup {
     const uint32_t *bkt;      // first contig-relative read index with pos >= b << BKT_SHIFT
     const int32_t *maxspan;   // [n_targets] max(endpos - pos)
     const uint32_t *cigar;    // padded by CIGAR_PAD zero words
+    const uint32_t *chunk;    // [arena words / CHUNK] chunk index (CH_POS | CH_DEL | CH_INS)
     int32_t n_targets;
 };
 
@@ -352,7 +364,7 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
         const bool slow = (rc.z & SLOW_BIT) != 0;
         const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
         const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op (multiple of OPL)
-        const int32_t en_pad = st0 + (int32_t)((ncig + (OPL - 1)) & ~(uint32_t)(OPL - 1));
+        const int32_t en_pad = st0 + (int32_t)((ncig + (ALIGN_OPS - 1)) & ~(uint32_t)(ALIGN_OPS - 1));
         const bool live = ovl && !slow && ncig > 0;
         const int nblk = (int)min<int64_t>(WAVE, hi - rb);
         const int32_t blk_end = rdlane_i(en_pad, nblk - 1);
@@ -503,6 +515,225 @@ __device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint3
                                    rdlane(clip, l), s, e, sink, st);
         }
     }
+    if (COUNT) st.ops += rdlane(wave_scan_add(live_ops), WAVE - 1);
+}
+
+// ------------------------------------------------------------------ index walk (default)
+// The chunk index (built once by svt_load_pileup) holds, for every CHUNK = 8 ops of the
+// padded arena, the reference walk position after the chunk's last op (refinement.c:141:
+// rp += len unless I/S) and two flags: the chunk holds a DEL candidate op (D, len > 50) /
+// an INS candidate op (I, len >= 50).  A window's walk then streams 4 B per 8 ops instead
+// of 32 B: positions are monotone inside a read, so the break of refinement.c:145 is the
+// first chunk whose end position exceeds inter.end (counted, not scanned), and only
+// chunks that hold a candidate op -- plus, for refine_end's leading-soft-clip candidate,
+// the chunk holding the break op -- are fetched op by op.  Those are queued in LDS as
+// {chunk, chunk start position} and resolved in batches (one 32-B load per lane).
+constexpr int EVCAP = 256;                  // queued chunks per wave before a flush
+constexpr uint32_t EV_STOP = 1u << 31;      // queued chunk holds the break op (refine_end soft clip)
+constexpr int ITILE = ALIGN_OPS * WAVE;     // 2048 ops (256 chunk words, 1 KiB) per index tile
+
+struct IndexLds {
+    int8_t slot[WAVE + 4];   // per tile lane slot: block-relative index of the read starting there, else -1
+    uint2 walk[WAVE];        // read k: {pos, stream-relative end of its real ops}
+    uint2 ev[EVCAP];         // queued chunks: {stream-relative chunk | EV_STOP, walk position before it}
+};
+
+__device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141: every op but I (1) and S (4)
+    return (w >> 4) & (uint32_t)__builtin_amdgcn_sbfe((int)~0x12u, w & 0xfu, 1);
+}
+
+// Resolve queued chunks: replay the reference walk over the chunk's 8 ops from its start
+// position; candidates are the ops before the break (refinement.c:124-145 / :190-206 /
+// :299-316), a STOP chunk also yields refine_end's soft-clip candidate rp + 1 (:210-220).
+template <int KIND>
+__device__ __forceinline__ void flush_chunks(const uint32_t *__restrict__ cg, IndexLds &L, int nev, uint32_t e,
+                                             Sink &sink) {
+    wave_sync();
+    for (int b = 0; b < nev; b += WAVE) {
+        const int i = b + lane_id();
+        if (i < nev) {
+            const uint2 en = L.ev[i];
+            const uint4 *src = reinterpret_cast<const uint4 *>(cg + (uint64_t)(en.x & ~EV_STOP) * CHUNK);
+            const uint4 c0 = src[0], c1 = src[1];
+            const uint32_t w[CHUNK] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            uint32_t rp = en.y;
+#pragma unroll
+            for (int k = 0; k < CHUNK; k++) {
+                const uint32_t op = w[k] & 0xfu, len = w[k] >> 4;
+                if (is_candidate_op<KIND>(op, len)) sink.push1(KIND == K_END ? (int32_t)(rp + len + 1u) : (int32_t)rp);
+                rp += ref_adv(w[k]);
+                if (rp > e) {
+                    if (KIND == K_END && (en.x & EV_STOP)) sink.push1((int32_t)(rp + 1u));
+                    break;
+                }
+            }
+        }
+    }
+    wave_sync();
+}
+
+template <int KIND, bool COUNT>
+__device__ __forceinline__ void gather_index(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
+                                             WinStats &st, IndexLds &L) {
+    // Chunk positions are < 2^30 for every read the index walk takes (the others are
+    // flagged slow at load time); windows ending at or past 2^31 take the exact per-read path.
+    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
+    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
+    int64_t lo, hi;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
+    const int ln = lane_id();
+    const uint64_t S0 = P.off64[lo];                 // multiple of ALIGN_OPS
+    const uint32_t base32 = (uint32_t)S0;
+    const uint32_t *cg = P.cigar + S0;               // stream-relative CIGAR words
+    const uint32_t *cx = P.chunk + S0 / CHUNK;        // stream-relative chunk words
+    uint32_t live_ops = 0;                            // COUNT builds
+    int nev = 0;                                      // queued chunks (wave-uniform)
+
+    for (int64_t rb = lo; rb < hi; rb += WAVE) {
+        // ---- one block of up to 64 reads, lane k <-> read rb + k
+        const int64_t r = rb + ln;
+        const bool inb = r < hi;
+        const uint4 rc = inb ? P.rec[r] : make_uint4(0, 0, 0, 0);
+        const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
+        const bool slow = (rc.z & SLOW_BIT) != 0;
+        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
+        const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op (multiple of 32)
+        const int32_t en_pad = st0 + (int32_t)((ncig + (ALIGN_OPS - 1)) & ~(uint32_t)(ALIGN_OPS - 1));
+        const bool live = ovl && !slow && ncig > 0;
+        const int nblk = (int)min<int64_t>(WAVE, hi - rb);
+        const int32_t blk_end = rdlane_i(en_pad, nblk - 1);
+        // refine_end's leading-soft-clip candidate needs the walk position after the break
+        // op (refinement.c:210-220): only reads with cigar[0] == S and s <= pos <= e
+        const bool need_stop = KIND == K_END && live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos &&
+                               (int64_t)rpos <= (int64_t)e;
+        const uint64_t stop_m = ballot(need_stop);
+        wave_sync();
+        L.walk[ln] = make_uint2(rpos, (uint32_t)(st0 + (int32_t)ncig));
+
+        // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
+        if (KIND != K_INS) {
+            const bool z = ovl && ncig == 0 && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
+            if (KIND == K_START) sink.push(z && (clip & SVT_CLIP_LAST_S), (int32_t)rpos);       // :152
+            else sink.push(z && (clip & SVT_CLIP_FIRST_S), (int32_t)(rpos + 1u));                // :210-220
+        }
+        if (COUNT) {
+            st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
+            if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
+        }
+
+        const uint64_t live_m = ballot(live);
+        const uint64_t clip_m = ballot(clip & SVT_CLIP_LAST_S);
+        int32_t J = live_m ? rdlane_i(st0, __builtin_ctzll(live_m)) : blk_end;
+        uint32_t carry_E = 0;
+        int32_t carry_k = -1;
+        uint4 cw = make_uint4(0, 0, 0, 0);
+        if (J < blk_end) cw = reinterpret_cast<const uint4 *>(cx + J / CHUNK)[ln];
+        while (J < blk_end) {
+            const int32_t A = J;                             // tiles start on a read start or a tile end
+            const int32_t U = min(A + ITILE, blk_end);
+            const int32_t jb = A + ALIGN_OPS * ln;           // this lane's first op
+            const bool lane_ok = jb < U;
+            // ---- which lanes start a read
+            L.slot[ln] = -1;
+            if (ln == 0) L.slot[WAVE] = -1;
+            wave_sync();
+            if (ncig > 0 && inb && st0 >= A && st0 <= A + ITILE) L.slot[(st0 - A) / ALIGN_OPS] = (int8_t)ln;
+            wave_sync();
+            const int32_t hk = lane_ok ? (int32_t)L.slot[ln] : -1;
+            const int32_t kinc = wave_scan_max(hk);
+            const int32_t kl = max(carry_k, kinc);           // this lane's read (>= 0 on every lane_ok lane)
+            const uint2 wk = L.walk[kl < 0 ? 0 : kl];       // {pos, real op end}
+            const uint32_t E[CPL] = {cw.x & CH_POS, cw.y & CH_POS, cw.z & CH_POS, cw.w & CH_POS};
+            const uint32_t F[CPL] = {cw.x, cw.y, cw.z, cw.w};
+            // walk position before this lane's first chunk: the read's pos at its head lane,
+            // else the previous lane's last chunk end (lane 0: the previous tile's)
+            const uint32_t prevE = dpp<0x138, 0xf>(E[CPL - 1]);   // wave_shr:1
+            const uint32_t start0 = hk >= 0 ? wk.x : (ln == 0 ? carry_E : prevE);
+
+            // ---- next tile: continue the read at U unless it already broke / yields nothing;
+            //      otherwise jump to the next read that yields.  Prefetch it now.
+            const int32_t next_carry_k = max(carry_k, rdlane_i(kinc, WAVE - 1));
+            const uint32_t next_carry_E = rdlane(E[CPL - 1], WAVE - 1);
+            int32_t Jn = U;
+            {
+                const int32_t kc = next_carry_k;
+                const bool cont = kc >= 0 && ((live_m >> kc) & 1ull) && U < rdlane_i(en_pad, kc) && next_carry_E <= e;
+                if (!cont) {
+                    const uint64_t later = kc >= 0 ? (live_m & ~((2ull << kc) - 1ull)) : live_m;
+                    Jn = later ? max(U, rdlane_i(st0, __builtin_ctzll(later))) : blk_end;
+                }
+            }
+            if (Jn < blk_end) cw = reinterpret_cast<const uint4 *>(cx + Jn / CHUNK)[ln];
+
+            // ---- this lane's chunks: [0, nb) end at or before inter.end; chunk nb (if real)
+            //      holds the break op (refinement.c:145); later chunks are dead.
+            const bool lane_live = lane_ok && kl >= 0 && ((live_m >> kl) & 1ull) && start0 <= e;
+            uint32_t nb = 0;
+#pragma unroll
+            for (int i = 0; i < CPL; i++) nb += E[i] <= e ? 1u : 0u;
+            const int32_t rem = (int32_t)wk.y - jb;                            // real ops from this lane on
+            const int32_t nreal_c = min(max(rem, 0) + CHUNK - 1, ALIGN_OPS + CHUNK - 1) / CHUNK;   // real chunks here
+            const bool brk = lane_live && (int32_t)nb < nreal_c;
+            const bool ends_here = rem > 0 && rem <= ALIGN_OPS;
+            const bool has_last = lane_live && ends_here && (int32_t)nb >= nreal_c;  // reached, no break
+            const uint32_t flag = KIND == K_INS ? CH_INS : CH_DEL;
+            const bool stop_q = KIND == K_END && brk && ((stop_m >> kl) & 1ull);
+            uint32_t qm = 0;
+            if (lane_live) {
+#pragma unroll
+                for (int i = 0; i < CPL; i++)
+                    if (i < nreal_c && (uint32_t)i <= nb && (F[i] & flag)) qm |= 1u << i;
+                if (stop_q) qm |= 1u << nb;
+            }
+            if (has_last) {
+                const uint32_t rp_end = E[nreal_c - 1];       // walk position after the read's last op
+                if (KIND == K_START) {   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
+                    if (((clip_m >> kl) & 1ull) && s <= rp_end) sink.push1((int32_t)rp_end);
+                } else if (KIND == K_END) {   // leading S, s <= pos <= e: rp + 1 (refinement.c:210-220)
+                    if ((stop_m >> kl) & 1ull) sink.push1((int32_t)(rp_end + 1u));
+                }
+            }
+            if (COUNT && lane_live) {
+                live_ops += (uint32_t)min((int32_t)nb * CHUNK, rem);
+                if (brk) {   // ops of the break chunk up to and including the break op
+                    const uint32_t *w = cg + jb + (int32_t)nb * CHUNK;
+                    uint32_t rp = nb ? E[nb - 1] : start0;
+                    int k = 0;
+                    while (k < CHUNK) { rp += ref_adv(w[k]); k++; if (rp > e) break; }
+                    live_ops += (uint32_t)k;
+                    if (KIND == K_START && jb + (int32_t)nb * CHUNK + k != (int32_t)wk.y) live_ops++;   // cigar[n-1] test
+                }
+            }
+            // ---- queue the chunks to resolve op by op (exclusive wave scan of per-lane counts)
+            const uint32_t nq = (uint32_t)__popc(qm);
+            const uint32_t incl = wave_scan_add(nq);
+            const int tot = (int)rdlane(incl, WAVE - 1);
+            if (tot) {
+                if (nev + tot > EVCAP) { flush_chunks<KIND>(cg, L, nev, e, sink); nev = 0; }
+                int o = nev + (int)(incl - nq);
+                uint32_t m = qm;
+                while (m) {
+                    const int i = __builtin_ctz(m);
+                    m &= m - 1;
+                    const uint32_t cs = i ? E[i - 1] : start0;   // walk position before chunk i
+                    L.ev[o++] = make_uint2((uint32_t)(jb / CHUNK + i) | (stop_q && (uint32_t)i == nb ? EV_STOP : 0u), cs);
+                }
+                nev += tot;
+            }
+            carry_E = next_carry_E;
+            carry_k = next_carry_k;
+            J = Jn;
+        }
+        // reads whose walk could leave the chunk index's range: exact per-read replay
+        uint64_t sm = ballot(ovl && slow);
+        while (sm) {
+            const int l = __builtin_ctzll(sm);
+            sm &= sm - 1;
+            walk_read<KIND, COUNT>(P.cigar, S0 + (uint64_t)(int64_t)rdlane_i(st0, l), rdlane(ncig, l), rdlane(rpos, l),
+                                   rdlane(clip, l), s, e, sink, st);
+        }
+    }
+    if (nev) flush_chunks<KIND>(cg, L, nev, e, sink);
     if (COUNT) st.ops += rdlane(wave_scan_add(live_ops), WAVE - 1);
 }
 
@@ -674,31 +905,35 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
 }
 
 struct WinLds {
-    union {                       // the stream scratch is dead once the vote starts
+    union {                       // the gather scratch is dead once the vote starts
         StreamLds sl;
+        IndexLds il;
         int64_t pre[CAP + 1];
     };
     int32_t cand[CAP];
     int32_t ncand;
 };
 
-template <int KIND, bool COUNT, bool STREAM>
+constexpr int G_PERREAD = 0, G_STREAM = 1, G_INDEX = 2;   // window gather variants (SVTREK_GATHER)
+
+template <int KIND, bool COUNT, int G>
 __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
-                                          StreamLds &L) {
+                                          WinLds &L) {
     if (lane_id() == 0) *sink.cnt = 0;
     wave_sync();
-    if (STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L);
+    if (G == G_INDEX) gather_index<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.il);
+    else if (G == G_STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.sl);
     else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
     wave_sync();
     return uniform_i(*sink.cnt);
 }
 
-template <int KIND, bool COUNT, bool STREAM, int VOTE = V_CONSENSUS>
+template <int KIND, bool COUNT, int G, int VOTE = V_CONSENSUS>
 __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e, uint32_t imprecise,
                                  unsigned long long *wk, int32_t &support) {
     WinStats st;
     Sink sink{lds.cand, CAP, &lds.ncand};
-    int32_t n = gather<KIND, COUNT, STREAM>(a, chrom - 1, s, e, sink, st, lds.sl);
+    int32_t n = gather<KIND, COUNT, G>(a, chrom - 1, s, e, sink, st, lds);
     if (COUNT && lane_id() == 0) {
         wk[0] += 1; wk[1] += st.reads; wk[2] += st.ops; wk[3] += (unsigned long long)n;
     }
@@ -721,7 +956,7 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     int64_t *gp = (int64_t *)(a.pool + ((base + (unsigned long long)N + 1ull) & ~1ull));
     WinStats st2;
     Sink s2{g, N, &lds.ncand};
-    gather<KIND, false, STREAM>(a, chrom - 1, s, e, s2, st2, lds.sl);
+    gather<KIND, false, G>(a, chrom - 1, s, e, s2, st2, lds);
     return sort_and_vote<VOTE>(g, gp, n, (int32_t)imprecise, a.prm, support);
 }
 
@@ -734,7 +969,7 @@ constexpr int WPB = 4;
 #define SVT_INTERLEAVE_WINDOWS 0
 #endif
 
-template <bool COUNT, bool STREAM>
+template <bool COUNT, int G>
 #ifndef SVT_WAVES_PER_EU
 #define SVT_WAVES_PER_EU 0       // 0: let the compiler choose (70 VGPRs -> 7 waves/SIMD)
 #endif
@@ -764,15 +999,15 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_kernel(KArgs a) {
     if (type == T_INS) {                                   // audit.c:176-187
         if (w == 0) {
             uint32_t s = pos - (uint32_t)k.median, e = pos + (uint32_t)k.median;
-            r = (uint32_t)refine_window<K_INS, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk, sup);
+            r = (uint32_t)refine_window<K_INS, COUNT, G>(a, lds, chrom, s, e, pos, wk, sup);
         }
     } else if (type == T_DEL) {                            // audit.c:188-220
         if (w == 0) {
             uint32_t s = pos - (uint32_t)k.wider, e = pos + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_START, COUNT, STREAM>(a, lds, chrom, s, e, pos, wk, sup);
+            r = (uint32_t)refine_window<K_START, COUNT, G>(a, lds, chrom, s, e, pos, wk, sup);
         } else {
             uint32_t s = end - (uint32_t)k.narrow, e = end + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_END, COUNT, STREAM>(a, lds, chrom, s, e, end, wk, sup);
+            r = (uint32_t)refine_window<K_END, COUNT, G>(a, lds, chrom, s, e, end, wk, sup);
         }
     }
     // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250), so both
@@ -790,6 +1025,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_kernel(KArgs a) {
 // is refine_ins's window exactly -- the same region query (sub_start-1, sub_end-1, :27),
 // the same walk (I >= 50 collects rp, advance unless I/S, break when rp > sub_end,
 // :30-54) -- so it reuses the stream gather; only the vote differs (sw_vote).
+template <int G>
 __global__ __launch_bounds__(64 * WPB) void sw_kernel(KArgs a) {
     __shared__ WinLds lds_all[WPB];
     const uint32_t wid = threadIdx.x >> 6;
@@ -800,7 +1036,7 @@ __global__ __launch_bounds__(64 * WPB) void sw_kernel(KArgs a) {
     const uint32_t s = (uint32_t)uniform_i((int32_t)q.y), e = (uint32_t)uniform_i((int32_t)q.z);
     unsigned long long wk[5];
     int32_t sup = 0;
-    const int32_t c = refine_window<K_INS, false, true, V_SLIDING>(a, lds_all[wid], chrom, s, e, 0u, wk, sup);
+    const int32_t c = refine_window<K_INS, false, G, V_SLIDING>(a, lds_all[wid], chrom, s, e, 0u, wk, sup);
     if (lane_id() == 0) a.sw_out[g] = make_int2(c, sup);
 }
 
@@ -817,27 +1053,43 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 }
 
 // svt_load_pileup's per-op work, on the device: one wave per read copies the read's
-// CIGAR words from the caller's unpadded layout into the padded arena (coalesced) and
-// sums the reference advance (refinement.c:141) to flag reads whose walk reaches 2^31
-// (SLOW_BIT: those take walk_read's exact uint32 replay).  The host only does per-read
-// work (offsets, prefix-max, buckets).
+// CIGAR words from the caller's unpadded layout into the padded arena (coalesced), and
+// builds the read's chunk index: for every CHUNK ops (zero padding up to ALIGN_OPS
+// included) the reference walk position after the chunk (refinement.c:141, a wave prefix
+// scan carried across 64-op steps) and the DEL/INS candidate flags.  Reads whose walk
+// reaches 2^30 (the chunk word's range) are flagged SLOW_BIT: those take walk_read's exact
+// uint32 replay.  The host only does per-read work (offsets, prefix-max, buckets).
 __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ raw, const uint64_t *__restrict__ raw_off,
                                                    const uint64_t *__restrict__ poff, uint4 *rec,
-                                                   uint32_t *__restrict__ arena, int64_t nr) {
+                                                   uint32_t *__restrict__ arena, uint32_t *__restrict__ chunk,
+                                                   int64_t nr) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= nr) return;
     const int ln = lane_id();
     const uint64_t o0 = raw_off[r], n = raw_off[r + 1] - o0, dst = poff[r];
+    const uint64_t npad = (n + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1);
+    const uint32_t rpos = rec[r].x;
     uint64_t walk = 0;
-    for (uint64_t i = (uint64_t)ln; i < n; i += WAVE) {
-        const uint32_t w = raw[o0 + i];
-        arena[dst + i] = w;
-        const uint32_t op = w & 0xfu;
-        if (op != OP_INS && op != OP_SOFT) walk += w >> 4;
+    uint32_t carry = rpos;
+    for (uint64_t i0 = 0; i0 < npad; i0 += WAVE) {
+        const uint64_t i = i0 + (uint64_t)ln;
+        const uint32_t w = i < n ? raw[o0 + i] : 0u;
+        if (i < n) arena[dst + i] = w;
+        const uint32_t adv = ref_adv(w);
+        walk += adv;
+        const uint32_t after = carry + wave_scan_add(adv);
+        const uint64_t dm = ballot(is_candidate_op<K_START>(w & 0xfu, w >> 4));
+        const uint64_t im = ballot(is_candidate_op<K_INS>(w & 0xfu, w >> 4));
+        if ((ln & (CHUNK - 1)) == CHUNK - 1 && i < npad) {
+            const int sh = ln & ~(CHUNK - 1);
+            chunk[(dst + i0) / CHUNK + (uint64_t)(ln / CHUNK)] =
+                (after & CH_POS) | (((dm >> sh) & 0xffull) ? CH_DEL : 0u) | (((im >> sh) & 0xffull) ? CH_INS : 0u);
+        }
+        carry = rdlane(after, WAVE - 1);
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) walk += __shfl_xor(walk, d, WAVE);
-    if (ln == 0 && (uint64_t)rec[r].x + walk >= (1ull << 31)) rec[r].z |= SLOW_BIT;
+    if (ln == 0 && (uint64_t)rpos + walk >= INDEX_LIMIT) rec[r].z |= SLOW_BIT;
 }
 
 }  // namespace
@@ -846,7 +1098,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
 struct svt_ctx {
     svt_params prm{};
     int device = 0;
-    bool stream_gather = true;    // SVTREK_GATHER=perread selects the per-read variant (A/B)
+    int gather = G_INDEX;         // SVTREK_GATHER=stream / perread select the A/B variants
     char err[512] = {0};
     // pileup
     int32_t n_targets = 0;
@@ -858,6 +1110,7 @@ struct svt_ctx {
     int64_t *d_tid_off = nullptr, *d_bkt_off = nullptr;
     uint32_t *d_bkt = nullptr;
     uint32_t *d_cigar = nullptr;
+    uint32_t *d_chunk = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
     // batch scratch
@@ -891,14 +1144,14 @@ void hfree(T *&p) {
 
 void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_maxspan); hfree(c->d_rec); hfree(c->d_off64);
-    hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
+    hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar); hfree(c->d_chunk);
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
-                       c->d_maxspan, c->d_cigar, c->n_targets};
+                       c->d_maxspan, c->d_cigar, c->d_chunk, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
                     c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
     a.loci = d_loci;
@@ -920,12 +1173,15 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 64, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
-    if (c->stream_gather) {
-        if (count) hipLaunchKernelGGL((refine_kernel<true, true>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((refine_kernel<false, true>), grid, block, 0, st, a);
+    if (c->gather == G_INDEX) {
+        if (count) hipLaunchKernelGGL((refine_kernel<true, G_INDEX>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((refine_kernel<false, G_INDEX>), grid, block, 0, st, a);
+    } else if (c->gather == G_STREAM) {
+        if (count) hipLaunchKernelGGL((refine_kernel<true, G_STREAM>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((refine_kernel<false, G_STREAM>), grid, block, 0, st, a);
     } else {
-        if (count) hipLaunchKernelGGL((refine_kernel<true, false>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((refine_kernel<false, false>), grid, block, 0, st, a);
+        if (count) hipLaunchKernelGGL((refine_kernel<true, G_PERREAD>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((refine_kernel<false, G_PERREAD>), grid, block, 0, st, a);
     }
     HIP_TRY(c, hipGetLastError());
     return SVT_OK;
@@ -967,7 +1223,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     if (!c) return SVT_ENOMEM;
     c->prm = *params;
     const char *g = getenv("SVTREK_GATHER");
-    c->stream_gather = !(g && strcmp(g, "perread") == 0);
+    c->gather = !g ? G_INDEX : strcmp(g, "perread") == 0 ? G_PERREAD : strcmp(g, "stream") == 0 ? G_STREAM : G_INDEX;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;
@@ -1009,7 +1265,7 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
 
     std::vector<int32_t> emax((size_t)nr), maxspan((size_t)(nt > 0 ? nt : 1), 0);
     std::vector<uint4> rec((size_t)nr);
-    std::vector<uint64_t> poff((size_t)nr + 1, 0);   // padded CIGAR offsets (multiples of OPL)
+    std::vector<uint64_t> poff((size_t)nr + 1, 0);   // padded CIGAR offsets (multiples of ALIGN_OPS)
     std::vector<int64_t> bkt_off((size_t)nt + 1, 0);
     std::vector<uint32_t> bkt;
     uint64_t pw = 0;
@@ -1029,7 +1285,7 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
             if (p->clip) clip = p->clip[r] & 3u;
             else clip = ncig ? (((p->cigar[o1 - 1] & 0xfu) == OP_SOFT ? 1u : 0u) |
                                 ((p->cigar[o0] & 0xfu) == OP_SOFT ? 2u : 0u)) : 0u;
-            // SLOW_BIT (walk >= 2^31) is set by pack_kernel on the device
+            // SLOW_BIT (walk reaching 2^30) is set by pack_kernel on the device
             if (p->endpos[r] > m) m = p->endpos[r];
             if (p->endpos[r] - p->pos[r] > ms) ms = p->endpos[r] - p->pos[r];
             maxpos = std::max(maxpos, p->pos[r]);
@@ -1037,7 +1293,7 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
             poff[(size_t)r] = pw;
             rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | (clip << 30),
                                         (uint32_t)pw);
-            pw += ((uint64_t)ncig + (OPL - 1)) & ~(uint64_t)(OPL - 1);
+            pw += ((uint64_t)ncig + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1);
         }
         if (r1 > r0 && pw - poff[(size_t)r0] >= (1ull << 31))
             return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^31 CIGAR ops on one contig");
@@ -1063,9 +1319,11 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
     if (nt > 0) { if ((s = upload(c, c->d_tid_off, p->tid_off, (size_t)nt + 1))) return s; }
     else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
-    // padded arena: read r's ops at poff[r], zero words (0M) up to the next multiple of OPL,
-    // then CIGAR_PAD zero words; filled on the device from the caller's unpadded words
+    // padded arena: read r's ops at poff[r], zero words (0M) up to the next multiple of
+    // ALIGN_OPS, then CIGAR_PAD zero words; filled on the device from the caller's unpadded
+    // words together with the chunk index (one word per CHUNK arena words)
     if ((s = upload<uint32_t>(c, c->d_cigar, nullptr, 0, (size_t)pw + CIGAR_PAD))) return s;
+    if ((s = upload<uint32_t>(c, c->d_chunk, nullptr, 0, (size_t)(pw / CHUNK) + CHUNK_PAD))) return s;
     if (nr > 0) {
         uint32_t *d_raw = nullptr;
         uint64_t *d_raw_off = nullptr;
@@ -1075,7 +1333,7 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
         if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, d_raw, d_raw_off,
-                               c->d_off64, c->d_rec, c->d_cigar, (int64_t)nr);
+                               c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, (int64_t)nr);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1196,7 +1454,10 @@ svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, i
             a.prm.sw_slide = slide_size;
             a.sw_sub = d_sub;
             a.sw_out = d_res;
-            hipLaunchKernelGGL(sw_kernel, dim3((unsigned)((ns + WPB - 1) / WPB)), dim3(64 * WPB), 0, nullptr, a);
+            const dim3 grid((unsigned)((ns + WPB - 1) / WPB)), block(64 * WPB);
+            if (c->gather == G_INDEX) hipLaunchKernelGGL(sw_kernel<G_INDEX>, grid, block, 0, nullptr, a);
+            else if (c->gather == G_STREAM) hipLaunchKernelGGL(sw_kernel<G_STREAM>, grid, block, 0, nullptr, a);
+            else hipLaunchKernelGGL(sw_kernel<G_PERREAD>, grid, block, 0, nullptr, a);
             chk(hipGetLastError(), "sw_kernel: %s");
         }
         if (s == SVT_OK) {

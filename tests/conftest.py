@@ -28,8 +28,9 @@ def engine_factory():
 
     engines = []
 
-    def make(params=None, gather="stream"):
-        """gather: "stream" (window-stream kernel, default) or "perread" (per-read walk variant)."""
+    def make(params=None, gather="index"):
+        """gather: "index" (chunk-index walk, default), "stream" (full CIGAR stream) or
+        "perread" (per-read walk) -- the SVTREK_GATHER variants of the engine."""
         old = os.environ.get("SVTREK_GATHER")
         os.environ["SVTREK_GATHER"] = gather
         try:

@@ -19,8 +19,8 @@ run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread; rc=$?
 tail -5 "$OUT/pytest.log"
 if [ $rc -gt 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
-run bench_stream 300 python bench.py --steps 20 --warmup 3 || exit $?
-tail -1 "$OUT/bench_stream.log"
-SVTREK_GATHER=perread run bench_perread 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
-tail -1 "$OUT/bench_perread.log"
+run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
+tail -1 "$OUT/bench.log"
+SVTREK_GATHER=stream run bench_streamvar 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
+tail -1 "$OUT/bench_streamvar.log"
 exit $rc
