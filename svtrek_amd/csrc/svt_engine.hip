@@ -35,7 +35,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.6.0 (gfx950, chunk-index walk)"
+#define SVT_VERSION "svtrek_amd 0.8.0 (gfx950, event walk)"
 
 namespace {
 
@@ -55,11 +55,12 @@ constexpr uint32_t CIGAR_PAD = 1040;        // zero words after the arena (tile 
 constexpr int CHUNK = 8;                    // ops per chunk
 constexpr int CPL = 4;                      // chunks per lane in the index walk
 constexpr int ALIGN_OPS = CHUNK * CPL;      // 32 ops: a lane's chunks belong to one read
-constexpr uint32_t CH_POS = 0x3fffffffu;    // chunk word: walk position after the chunk's last op
+constexpr uint32_t CH_POS = 0x1fffffffu;    // chunk word: walk position after the chunk's last op
+constexpr uint32_t CH_HEAD = 1u << 29;      //   the chunk is a read's first chunk
 constexpr uint32_t CH_DEL = 1u << 30;       //   the chunk holds a D op with len > 50  (refinement.c:124,:190)
 constexpr uint32_t CH_INS = 1u << 31;       //   the chunk holds an I op with len >= 50 (refinement.c:299)
-constexpr uint32_t CHUNK_PAD = 272;         // zero words after the chunk index (tile over-read)
-constexpr uint64_t INDEX_LIMIT = 1ull << 30; // walks reaching 2^30 are flagged slow (chunk word has 30 bits)
+constexpr uint32_t CHUNK_PAD = 1040;        // zero words after the chunk index (speculative tile over-read)
+constexpr uint64_t INDEX_LIMIT = 1ull << 29; // walks reaching 2^29 are flagged slow (chunk word has 29 position bits)
 
 struct DevPileup {
     const int32_t *pos;       // [n_reads]
@@ -68,10 +69,11 @@ struct DevPileup {
     const uint64_t *off64;    // [n_reads+1] cig_off
     const int64_t *tid_off;   // [n_targets+1]
     const int64_t *bkt_off;   // [n_targets+1] start of each contig's bucket table
-    const uint32_t *bkt;      // first contig-relative read index with pos >= b << BKT_SHIFT
-    const int32_t *maxspan;   // [n_targets] max(endpos - pos)
+    const uint2 *bkt;         // {first read with pos >= b << BKT_SHIFT, first read with emax >= b << BKT_SHIFT}
     const uint32_t *cigar;    // padded by CIGAR_PAD zero words
-    const uint32_t *chunk;    // [arena words / CHUNK] chunk index (CH_POS | CH_DEL | CH_INS)
+    const uint32_t *chunk;    // [arena words / CHUNK] chunk index (CH_POS | CH_HEAD | CH_DEL | CH_INS)
+    const uint4 *rec2;        // [n_reads] {walk end, candidate-op count, event offset lo, hi}
+    const uint2 *ev;          // candidate ops of every read in op order: {walk position before the op, CIGAR word}
     int32_t n_targets;
 };
 
@@ -267,28 +269,35 @@ __device__ __forceinline__ void walk_read(const uint32_t *__restrict__ cigar, ui
 }
 
 // ------------------------------------------------------------------ read range (A3)
-// First contig-relative read index with pos >= X (X >= 0), via the bucket table.
-__device__ __forceinline__ int64_t first_pos_ge(const DevPileup &P, int tid, int64_t ra, int64_t nr, int64_t X) {
-    const int64_t b0 = P.bkt_off[tid], nb = P.bkt_off[tid + 1] - b0;
-    int64_t b = X >> BKT_SHIFT;
-    if (b >= nb - 1) return nr;                 // past the last read start
-    int64_t l = P.bkt[b0 + b], h = P.bkt[b0 + b + 1];
-    const int32_t *pos = P.pos + ra;
-    return wave_partition_point(l, h, [&](int64_t r) { return (int64_t)pos[r] >= X; });
+// sam_itr_queryi(idx, chrom-1, inter.start-1, inter.end-1) (refinement.c:114): the reads
+// [lo, hi) of contig tid may overlap [beg, end) (each still needs endpos > beg), with
+//   hi = first read with pos >= end,  lo = first read with emax > beg  (emax = prefix max
+//   of endpos, so every read before lo ends at or before beg).
+// The bucket table gives, per 4 kb bucket b, {first read with pos >= b*4096, first read with
+// emax >= b*4096}; each bound then lies inside one bucket, and the two searches share two
+// dependent steps: 4 bucket words, then one 64-lane probe each of pos[] and emax[].
+__device__ __forceinline__ int64_t probe_first(int64_t l, int64_t h, bool hit_in_lane, bool lane_valid) {
+    const uint64_t m = ballot(lane_valid && hit_in_lane);
+    return m ? l + __builtin_ctzll(m) : h;
 }
 
-// sam_itr_queryi(idx, chrom-1, inter.start-1, inter.end-1) (refinement.c:114): the
-// reads [lo, hi) of contig tid may overlap [beg, end); each still needs endpos > beg.
 __device__ __forceinline__ bool read_range(const DevPileup &P, int tid, int64_t beg, int64_t end, int64_t &lo,
                                            int64_t &hi) {
     if (tid < 0 || tid >= P.n_targets || end <= beg) return false;   // no reads (A3)
     const int64_t ra = P.tid_off[tid], nr = P.tid_off[tid + 1] - ra;
     if (nr == 0) return false;
-    int64_t h = first_pos_ge(P, tid, ra, nr, end);
-    int64_t lb = beg - (int64_t)P.maxspan[tid];
-    int64_t l0 = lb > 0 ? first_pos_ge(P, tid, ra, nr, lb) : 0;
-    const int32_t *emax = P.emax + ra;
-    int64_t l = wave_partition_point(l0, h, [&](int64_t r) { return (int64_t)emax[r] > beg; });
+    const int64_t b0 = P.bkt_off[tid], nb = P.bkt_off[tid + 1] - b0;   // last bucket = {nr, nr}
+    const int ln = lane_id();
+    const int64_t bi = min((ln < 2 ? end >> BKT_SHIFT : beg >> BKT_SHIFT) + (ln & 1), nb - 1);
+    const uint2 bw = ln < 4 ? P.bkt[b0 + bi] : make_uint2(0, 0);
+    const int64_t hl = rdlane(bw.x, 0), hh = rdlane(bw.x, 1), ll = rdlane(bw.y, 2), lh = rdlane(bw.y, 3);
+    const int32_t *pos = P.pos + ra, *emax = P.emax + ra;
+    const bool vh = hl + ln < hh, vl = ll + ln < lh;
+    const int32_t pv = vh ? pos[hl + ln] : 0, ev = vl ? emax[ll + ln] : 0;
+    int64_t h = probe_first(hl, hh, (int64_t)pv >= end, vh);
+    int64_t l = probe_first(ll, lh, (int64_t)ev > beg, vl);
+    if (hh - hl > WAVE) h = wave_partition_point(hl, hh, [&](int64_t r) { return (int64_t)pos[r] >= end; });
+    if (lh - ll > WAVE) l = wave_partition_point(ll, lh, [&](int64_t r) { return (int64_t)emax[r] > beg; });
     lo = ra + l;
     hi = ra + h;
     return lo < hi;
@@ -532,11 +541,16 @@ constexpr int EVCAP = 256;                  // queued chunks per wave before a f
 constexpr uint32_t EV_STOP = 1u << 31;      // queued chunk holds the break op (refine_end soft clip)
 constexpr int ITILE = ALIGN_OPS * WAVE;     // 2048 ops (256 chunk words, 1 KiB) per index tile
 
+constexpr uint32_t RD_LIVE = 1u, RD_STOP = 2u, RD_CLIPL = 4u;   // IndexLds::rd[k].y flags (| clip << 30)
+
 struct IndexLds {
-    int8_t slot[WAVE + 4];   // per tile lane slot: block-relative index of the read starting there, else -1
-    uint2 walk[WAVE];        // read k: {pos, stream-relative end of its real ops}
+    uint4 rd[WAVE];          // read k of the block: {pos, RD_* flags | clip << 30, stream-relative end of its
+                             //   real ops, stream-relative first op}
     uint2 ev[EVCAP];         // queued chunks: {stream-relative chunk | EV_STOP, walk position before it}
+    int32_t nev;             // queued chunk count (LDS-atomic slot allocation)
 };
+
+__device__ __forceinline__ uint32_t cw_word(const uint4 &v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 
 __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141: every op but I (1) and S (4)
     return (w >> 4) & (uint32_t)__builtin_amdgcn_sbfe((int)~0x12u, w & 0xfu, 1);
@@ -545,30 +559,51 @@ __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141:
 // Resolve queued chunks: replay the reference walk over the chunk's 8 ops from its start
 // position; candidates are the ops before the break (refinement.c:124-145 / :190-206 /
 // :299-316), a STOP chunk also yields refine_end's soft-clip candidate rp + 1 (:210-220).
-template <int KIND>
+#ifndef SVT_RN
+#define SVT_RN 0                 // 1: prefetch the next block's records
+#endif
+#ifndef SVT_QSCAN
+#define SVT_QSCAN 0              // 1: queue slots from a wave prefix scan instead of LDS atomics
+#endif
+#ifndef SVT_DIAG
+#define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 2 = no chunk resolve
+#endif
+// LEAN: the mid-tile overflow flush (rare), which must leave the walk's registers alone:
+// one 16-B half of the chunk in flight at a time.
+template <int KIND, bool LEAN>
 __device__ __forceinline__ void flush_chunks(const uint32_t *__restrict__ cg, IndexLds &L, int nev, uint32_t e,
                                              Sink &sink) {
+    if (SVT_DIAG == 2) return;
     wave_sync();
     for (int b = 0; b < nev; b += WAVE) {
         const int i = b + lane_id();
         if (i < nev) {
             const uint2 en = L.ev[i];
             const uint4 *src = reinterpret_cast<const uint4 *>(cg + (uint64_t)(en.x & ~EV_STOP) * CHUNK);
-            const uint4 c0 = src[0], c1 = src[1];
-            const uint32_t w[CHUNK] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
             uint32_t rp = en.y;
+            bool done = false;
+            uint4 c1 = make_uint4(0, 0, 0, 0);
+            if (!LEAN) c1 = src[1];
 #pragma unroll
-            for (int k = 0; k < CHUNK; k++) {
-                const uint32_t op = w[k] & 0xfu, len = w[k] >> 4;
-                if (is_candidate_op<KIND>(op, len)) sink.push1(KIND == K_END ? (int32_t)(rp + len + 1u) : (int32_t)rp);
-                rp += ref_adv(w[k]);
-                if (rp > e) {
-                    if (KIND == K_END && (en.x & EV_STOP)) sink.push1((int32_t)(rp + 1u));
-                    break;
+            for (int h = 0; h < 2 && !done; h++) {
+                const uint4 c = h == 0 ? src[0] : (LEAN ? src[1] : c1);
+                const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t op = w[k] & 0xfu, len = w[k] >> 4;
+                    if (is_candidate_op<KIND>(op, len)) sink.push1(KIND == K_END ? (int32_t)(rp + len + 1u) : (int32_t)rp);
+                    rp += ref_adv(w[k]);
+                    if (rp > e) {
+                        if (KIND == K_END && (en.x & EV_STOP)) sink.push1((int32_t)(rp + 1u));
+                        done = true;
+                        break;
+                    }
                 }
             }
         }
     }
+    wave_sync();
+    if (lane_id() == 0) L.nev = 0;
     wave_sync();
 }
 
@@ -581,35 +616,47 @@ __device__ __forceinline__ void gather_index(const DevPileup &P, int tid, uint32
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
     if (!read_range(P, tid, beg, end, lo, hi)) return;
+#if SVT_DIAG == 1
+    if (lo < hi) return;          // diagnostic build: region query only
+#endif
     const int ln = lane_id();
+    // one dependent step: the stream base and the first block's records
     const uint64_t S0 = P.off64[lo];                 // multiple of ALIGN_OPS
+    int64_t rb = lo;
+    uint4 rc = rb + ln < hi ? P.rec[rb + ln] : make_uint4(0, 0, 0, 0);
+#if SVT_RN
+    uint4 rn = rb + WAVE + ln < hi ? P.rec[rb + WAVE + ln] : make_uint4(0, 0, 0, 0);
+#endif
     const uint32_t base32 = (uint32_t)S0;
     const uint32_t *cg = P.cigar + S0;               // stream-relative CIGAR words
     const uint32_t *cx = P.chunk + S0 / CHUNK;        // stream-relative chunk words
     uint32_t live_ops = 0;                            // COUNT builds
     int nev = 0;                                      // queued chunks (wave-uniform)
 
-    for (int64_t rb = lo; rb < hi; rb += WAVE) {
-        // ---- one block of up to 64 reads, lane k <-> read rb + k
-        const int64_t r = rb + ln;
-        const bool inb = r < hi;
-        const uint4 rc = inb ? P.rec[r] : make_uint4(0, 0, 0, 0);
+    // ---- per-block state: lane k <-> read rb + k
+    int32_t st0 = 0, en_pad = 0, blk_end = 0, J = 0, Rb = -1;
+    uint64_t live_m = 0, slow_m = 0;
+    uint32_t carry_E = 0;
+    if (ln == 0) L.nev = 0;
+    auto open_block = [&]() {
+        const bool inb = rb + ln < hi;
         const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
         const bool slow = (rc.z & SLOW_BIT) != 0;
-        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
-        const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op (multiple of 32)
-        const int32_t en_pad = st0 + (int32_t)((ncig + (ALIGN_OPS - 1)) & ~(uint32_t)(ALIGN_OPS - 1));
+        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;  // hts_itr_next overlap; pos < end below hi
+        st0 = (int32_t)(rc.w - base32);                        // stream-relative first op (multiple of 32)
+        en_pad = st0 + (int32_t)max((ncig + (ALIGN_OPS - 1)) & ~(uint32_t)(ALIGN_OPS - 1), (uint32_t)ALIGN_OPS);
         const bool live = ovl && !slow && ncig > 0;
         const int nblk = (int)min<int64_t>(WAVE, hi - rb);
-        const int32_t blk_end = rdlane_i(en_pad, nblk - 1);
+        blk_end = rdlane_i(en_pad, nblk - 1);
         // refine_end's leading-soft-clip candidate needs the walk position after the break
         // op (refinement.c:210-220): only reads with cigar[0] == S and s <= pos <= e
-        const bool need_stop = KIND == K_END && live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos &&
-                               (int64_t)rpos <= (int64_t)e;
-        const uint64_t stop_m = ballot(need_stop);
+        const bool stop = KIND == K_END && live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos &&
+                          (int64_t)rpos <= (int64_t)e;
+        const bool clipl = KIND == K_START && (clip & SVT_CLIP_LAST_S);
         wave_sync();
-        L.walk[ln] = make_uint2(rpos, (uint32_t)(st0 + (int32_t)ncig));
-
+        L.rd[ln] = make_uint4(rpos, (live ? RD_LIVE : 0u) | (stop ? RD_STOP : 0u) | (clipl ? RD_CLIPL : 0u) | (clip << 30),
+                              (uint32_t)(st0 + (int32_t)ncig), (uint32_t)st0);
+        wave_sync();
         // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
         if (KIND != K_INS) {
             const bool z = ovl && ncig == 0 && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
@@ -620,97 +667,141 @@ __device__ __forceinline__ void gather_index(const DevPileup &P, int tid, uint32
             st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
             if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
         }
+        live_m = ballot(live);
+        slow_m = ballot(ovl && slow);
+        if (live_m) {
+            const int k0 = __builtin_ctzll(live_m);
+            J = rdlane_i(st0, k0);
+            Rb = k0 - 1;
+        } else {
+            J = blk_end;
+        }
+        carry_E = 0;
+    };
+    auto close_block = [&]() {
+        // reads whose walk could leave the chunk index's range: exact per-read replay
+        uint64_t sm = slow_m;
+        while (sm) {
+            const int l = __builtin_ctzll(sm);
+            sm &= sm - 1;
+            const uint4 q = L.rd[l];
+            walk_read<KIND, COUNT>(P.cigar, S0 + (uint64_t)q.w, uniform_i((int32_t)(q.z - q.w)), uniform_i((int32_t)q.x),
+                                   uniform_i((int32_t)(q.y >> 30)), s, e, sink, st);
+        }
+    };
+    // Move to the next block holding a read that yields; false when the window is done.
+    auto next_block = [&]() -> bool {
+        for (;;) {
+            close_block();
+            rb += WAVE;
+            if (rb >= hi) return false;
+#if SVT_RN
+            rc = rn;
+            rn = rb + WAVE + ln < hi ? P.rec[rb + WAVE + ln] : make_uint4(0, 0, 0, 0);
+#else
+            rc = rb + ln < hi ? P.rec[rb + ln] : make_uint4(0, 0, 0, 0);
+#endif
+            open_block();
+            if (J < blk_end) return true;
+        }
+    };
+    auto load_tile = [&](int32_t at) { return reinterpret_cast<const uint4 *>(cx + at / CHUNK)[ln]; };
 
-        const uint64_t live_m = ballot(live);
-        const uint64_t clip_m = ballot(clip & SVT_CLIP_LAST_S);
-        int32_t J = live_m ? rdlane_i(st0, __builtin_ctzll(live_m)) : blk_end;
-        uint32_t carry_E = 0;
-        int32_t carry_k = -1;
-        uint4 cw = make_uint4(0, 0, 0, 0);
-        if (J < blk_end) cw = reinterpret_cast<const uint4 *>(cx + J / CHUNK)[ln];
-        while (J < blk_end) {
-            const int32_t A = J;                             // tiles start on a read start or a tile end
-            const int32_t U = min(A + ITILE, blk_end);
-            const int32_t jb = A + ALIGN_OPS * ln;           // this lane's first op
-            const bool lane_ok = jb < U;
-            // ---- which lanes start a read
-            L.slot[ln] = -1;
-            if (ln == 0) L.slot[WAVE] = -1;
-            wave_sync();
-            if (ncig > 0 && inb && st0 >= A && st0 <= A + ITILE) L.slot[(st0 - A) / ALIGN_OPS] = (int8_t)ln;
-            wave_sync();
-            const int32_t hk = lane_ok ? (int32_t)L.slot[ln] : -1;
-            const int32_t kinc = wave_scan_max(hk);
-            const int32_t kl = max(carry_k, kinc);           // this lane's read (>= 0 on every lane_ok lane)
-            const uint2 wk = L.walk[kl < 0 ? 0 : kl];       // {pos, real op end}
-            const uint32_t E[CPL] = {cw.x & CH_POS, cw.y & CH_POS, cw.z & CH_POS, cw.w & CH_POS};
-            const uint32_t F[CPL] = {cw.x, cw.y, cw.z, cw.w};
-            // walk position before this lane's first chunk: the read's pos at its head lane,
-            // else the previous lane's last chunk end (lane 0: the previous tile's)
-            const uint32_t prevE = dpp<0x138, 0xf>(E[CPL - 1]);   // wave_shr:1
-            const uint32_t start0 = hk >= 0 ? wk.x : (ln == 0 ? carry_E : prevE);
+    // One tile [J, U = min(J + ITILE, blk_end)) from `cw`; sets J to the next tile's start
+    // (or blk_end when the block is finished).  Every read occupies whole 32-op lane groups
+    // whose first chunk carries CH_HEAD, so a lane's read is Rb + (heads at lanes <= it).
+    auto tile = [&](const uint4 cw) {
+        const int32_t A = J;
+        const int32_t U = min(A + ITILE, blk_end);
+        const int32_t jb = A + ALIGN_OPS * ln;           // this lane's first op
+        const int nok = (U - A) / ALIGN_OPS;             // lanes inside the tile (1..64)
+        const bool lane_ok = ln < nok;
+        const bool head = lane_ok && (cw.x & CH_HEAD);
+        const uint64_t hm = ballot(head);
+        const int32_t kl = Rb + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u)) +
+                           (head ? 1 : 0);
+        const uint2 wk = reinterpret_cast<const uint2 *>(&L.rd[lane_ok ? kl : 0])[0];   // {pos, RD_* flags}
+        const uint32_t E[CPL] = {cw.x & CH_POS, cw.y & CH_POS, cw.z & CH_POS, cw.w & CH_POS};
+        // walk position before this lane's first chunk: the read's pos at its head lane,
+        // else the previous lane's last chunk end (lane 0: the previous tile's)
+        const uint32_t prevE = dpp<0x138, 0xf>(E[CPL - 1]);   // wave_shr:1
+        const uint32_t start0 = head ? wk.x : (ln == 0 ? carry_E : prevE);
 
-            // ---- next tile: continue the read at U unless it already broke / yields nothing;
-            //      otherwise jump to the next read that yields.  Prefetch it now.
-            const int32_t next_carry_k = max(carry_k, rdlane_i(kinc, WAVE - 1));
-            const uint32_t next_carry_E = rdlane(E[CPL - 1], WAVE - 1);
-            int32_t Jn = U;
+        // ---- next tile: continue the read at U unless it already broke / yields nothing;
+        //      otherwise jump to the next read that yields (its first group is a head)
+        const int32_t kc = rdlane_i(kl, nok - 1);                 // read holding the last op before U
+        const uint32_t E_U = rdlane(E[CPL - 1], nok - 1);          // its walk position at U
+        const bool U_end = U == blk_end || U == rdlane_i(en_pad, kc);
+        int32_t Jn, Rn = kc;
+        if (!U_end && ((live_m >> kc) & 1ull) && E_U <= e) {
+            Jn = U;
+        } else {
+            const uint64_t later = live_m & ~((2ull << kc) - 1ull);
+            if (later) {
+                const int kn = __builtin_ctzll(later);
+                Jn = rdlane_i(st0, kn);
+                Rn = kn - 1;
+            } else {
+                Jn = blk_end;
+            }
+        }
+
+        // ---- this lane's chunks: [0, nb) end at or before inter.end; chunk nb (if any)
+        //      holds the break op (refinement.c:145); later chunks are dead.  Padding chunks
+        //      repeat the read's last position, so a chunk ending past inter.end is real.
+        const bool lane_live = lane_ok && (wk.y & RD_LIVE) && start0 <= e;
+        uint32_t nb = 0;
+#pragma unroll
+        for (int i = 0; i < CPL; i++) nb += E[i] <= e ? 1u : 0u;
+        const bool brk = lane_live && nb < (uint32_t)CPL;
+        // the read's last lane group: the next group starts a read (or U ends it)
+        const bool next_head = ln + 1 < nok ? ((hm >> (ln + 1)) & 1ull) != 0 : (ln + 1 == nok && U_end);
+        const bool has_last = lane_live && next_head && nb == (uint32_t)CPL;   // reached, no break
+        const uint32_t flag = KIND == K_INS ? CH_INS : CH_DEL;
+        const bool stop_q = KIND == K_END && brk && (wk.y & RD_STOP);
+        uint32_t qm = 0;
+        if (lane_live) {
+#pragma unroll
+            for (int i = 0; i < CPL; i++)
+                if ((uint32_t)i <= nb && (cw_word(cw, i) & flag)) qm |= 1u << i;
+            if (stop_q) qm |= 1u << nb;
+        }
+        if (has_last) {
+            const uint32_t rp_end = E[CPL - 1];           // walk position after the read's last op
+            if (KIND == K_START) {   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
+                if ((wk.y & RD_CLIPL) && s <= rp_end) sink.push1((int32_t)rp_end);
+            } else if (KIND == K_END) {   // leading S, s <= pos <= e: rp + 1 (refinement.c:210-220)
+                if (wk.y & RD_STOP) sink.push1((int32_t)(rp_end + 1u));
+            }
+        }
+        if (COUNT && lane_live) {
+            const int32_t wz = (int32_t)L.rd[kl].z;                         // real op end
+            const int32_t rem = wz - jb;                                   // real ops from this lane on
+            live_ops += (uint32_t)min((int32_t)nb * CHUNK, rem);
+            if (brk) {   // ops of the break chunk up to and including the break op
+                const uint32_t *w = cg + jb + (int32_t)nb * CHUNK;
+                uint32_t rp = nb ? E[nb - 1] : start0;
+                int k = 0;
+                while (k < CHUNK) { rp += ref_adv(w[k]); k++; if (rp > e) break; }
+                live_ops += (uint32_t)k;
+                if (KIND == K_START && jb + (int32_t)nb * CHUNK + k != wz) live_ops++;   // cigar[n-1] test
+            }
+        }
+        // ---- queue the chunks to resolve op by op (slots from an LDS atomic counter)
+        if (ballot(qm != 0)) {
+            int tot = 0;
+#pragma unroll
+            for (int i = 0; i < CPL; i++) tot += __popcll(ballot((qm >> i) & 1u));
+            if (nev + tot > EVCAP) { flush_chunks<KIND, true>(cg, L, nev, e, sink); nev = 0; }
+#if SVT_QSCAN
             {
-                const int32_t kc = next_carry_k;
-                const bool cont = kc >= 0 && ((live_m >> kc) & 1ull) && U < rdlane_i(en_pad, kc) && next_carry_E <= e;
-                if (!cont) {
-                    const uint64_t later = kc >= 0 ? (live_m & ~((2ull << kc) - 1ull)) : live_m;
-                    Jn = later ? max(U, rdlane_i(st0, __builtin_ctzll(later))) : blk_end;
-                }
-            }
-            if (Jn < blk_end) cw = reinterpret_cast<const uint4 *>(cx + Jn / CHUNK)[ln];
-
-            // ---- this lane's chunks: [0, nb) end at or before inter.end; chunk nb (if real)
-            //      holds the break op (refinement.c:145); later chunks are dead.
-            const bool lane_live = lane_ok && kl >= 0 && ((live_m >> kl) & 1ull) && start0 <= e;
-            uint32_t nb = 0;
-#pragma unroll
-            for (int i = 0; i < CPL; i++) nb += E[i] <= e ? 1u : 0u;
-            const int32_t rem = (int32_t)wk.y - jb;                            // real ops from this lane on
-            const int32_t nreal_c = min(max(rem, 0) + CHUNK - 1, ALIGN_OPS + CHUNK - 1) / CHUNK;   // real chunks here
-            const bool brk = lane_live && (int32_t)nb < nreal_c;
-            const bool ends_here = rem > 0 && rem <= ALIGN_OPS;
-            const bool has_last = lane_live && ends_here && (int32_t)nb >= nreal_c;  // reached, no break
-            const uint32_t flag = KIND == K_INS ? CH_INS : CH_DEL;
-            const bool stop_q = KIND == K_END && brk && ((stop_m >> kl) & 1ull);
-            uint32_t qm = 0;
-            if (lane_live) {
-#pragma unroll
-                for (int i = 0; i < CPL; i++)
-                    if (i < nreal_c && (uint32_t)i <= nb && (F[i] & flag)) qm |= 1u << i;
-                if (stop_q) qm |= 1u << nb;
-            }
-            if (has_last) {
-                const uint32_t rp_end = E[nreal_c - 1];       // walk position after the read's last op
-                if (KIND == K_START) {   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
-                    if (((clip_m >> kl) & 1ull) && s <= rp_end) sink.push1((int32_t)rp_end);
-                } else if (KIND == K_END) {   // leading S, s <= pos <= e: rp + 1 (refinement.c:210-220)
-                    if ((stop_m >> kl) & 1ull) sink.push1((int32_t)(rp_end + 1u));
-                }
-            }
-            if (COUNT && lane_live) {
-                live_ops += (uint32_t)min((int32_t)nb * CHUNK, rem);
-                if (brk) {   // ops of the break chunk up to and including the break op
-                    const uint32_t *w = cg + jb + (int32_t)nb * CHUNK;
-                    uint32_t rp = nb ? E[nb - 1] : start0;
-                    int k = 0;
-                    while (k < CHUNK) { rp += ref_adv(w[k]); k++; if (rp > e) break; }
-                    live_ops += (uint32_t)k;
-                    if (KIND == K_START && jb + (int32_t)nb * CHUNK + k != (int32_t)wk.y) live_ops++;   // cigar[n-1] test
-                }
-            }
-            // ---- queue the chunks to resolve op by op (exclusive wave scan of per-lane counts)
-            const uint32_t nq = (uint32_t)__popc(qm);
-            const uint32_t incl = wave_scan_add(nq);
-            const int tot = (int)rdlane(incl, WAVE - 1);
-            if (tot) {
-                if (nev + tot > EVCAP) { flush_chunks<KIND>(cg, L, nev, e, sink); nev = 0; }
-                int o = nev + (int)(incl - nq);
+                const uint32_t nq = (uint32_t)__popc(qm);
+                int o = nev + (int)(wave_scan_add(nq) - nq);
+#else
+            if (qm) {
+                int o = atomicAdd(&L.nev, __popc(qm));
+#endif
                 uint32_t m = qm;
                 while (m) {
                     const int i = __builtin_ctz(m);
@@ -718,23 +809,196 @@ __device__ __forceinline__ void gather_index(const DevPileup &P, int tid, uint32
                     const uint32_t cs = i ? E[i - 1] : start0;   // walk position before chunk i
                     L.ev[o++] = make_uint2((uint32_t)(jb / CHUNK + i) | (stop_q && (uint32_t)i == nb ? EV_STOP : 0u), cs);
                 }
-                nev += tot;
             }
-            carry_E = next_carry_E;
-            carry_k = next_carry_k;
-            J = Jn;
+            nev += tot;
         }
-        // reads whose walk could leave the chunk index's range: exact per-read replay
+        carry_E = E_U;
+        Rb = Rn;
+        J = Jn;
+    };
+
+    // Two tile buffers in flight (ping-pong, static registers): while one tile is walked, the
+    // next one's chunk words (exact, or a guess that the stream continues contiguously, into
+    // the next block too) are already loading; a wrong guess costs one reload.
+    open_block();
+    if (J >= blk_end && !next_block()) { if (nev) flush_chunks<KIND, false>(cg, L, nev, e, sink); return; }
+    uint4 b0 = load_tile(J), b1;
+    int32_t t1;
+    {
+        const int32_t g = min(J + ITILE, blk_end);
+        b1 = load_tile(g);
+        t1 = g;
+    }
+    int32_t t0 = J;
+    // step: walk `cur` (holds tile J); make `nxt` hold the next tile, refill `cur` with a guess
+    auto step = [&](uint4 &cur, int32_t &tc, uint4 &nxt, int32_t &tn) -> bool {
+        tile(cur);
+        if (J >= blk_end && !next_block()) return false;
+        if (tn != J) { nxt = load_tile(J); tn = J; }
+        const int32_t g = min(J + ITILE, blk_end);
+        cur = load_tile(g);
+        tc = g;
+        return true;
+    };
+    (void)t0;
+    for (;;) {
+        if (!step(b0, t0, b1, t1)) break;
+        if (!step(b1, t1, b0, t0)) break;
+    }
+    if (nev) flush_chunks<KIND, false>(cg, L, nev, e, sink);
+    if (COUNT) st.ops += rdlane(wave_scan_add(live_ops), WAVE - 1);
+}
+
+// ------------------------------------------------------------------ event walk (default)
+// A read's walk (refinement.c:118-159 / :184-221 / :295-318) only matters to the vote
+// through (1) its candidate ops processed before the break and (2) the walk position at the
+// break or at the end, for the soft-clip candidates.  Both come from per-read summaries built
+// once by svt_load_pileup, independent of any query:
+//   * the read's candidate ops in op order, each with the walk position before it (`ev`):
+//     op i is processed iff that position is <= inter.end (positions only grow along the
+//     read, refinement.c:145), so a window takes the prefix of the list at or below inter.end;
+//   * the walk end (rec2.x): the read breaks iff walk end > inter.end;
+//   * the chunk index, searched (one 64-lane probe per 256 chunks) only when refine_end needs
+//     the position after the break op (leading soft clip, refinement.c:210-220) or when the
+//     work is counted.
+// So a window costs O(reads + candidate ops), independent of CIGAR length.
+
+// Walk position after the break op of a read that breaks (walk end > e): the first op whose
+// walk position after it exceeds e.  Wave-cooperative, uniform arguments; `op_idx` receives
+// the break op's index in the read.
+__device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0, uint32_t ncig, uint32_t rpos,
+                                                uint32_t e, uint32_t &op_idx) {
+    const int ln = lane_id();
+    const uint64_t c0 = op0 / CHUNK;
+    const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
+    uint32_t bc = nch, before = rpos;   // break chunk, walk position before it
+    for (uint32_t b = 0; b < nch; b += 4 * WAVE) {
+        const uint32_t c = b + 4u * (uint32_t)ln;
+        const uint4 q = c < nch ? *reinterpret_cast<const uint4 *>(P.chunk + c0 + c) : make_uint4(0, 0, 0, 0);
+        const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
+        uint32_t first = 4;
+#pragma unroll
+        for (int i = 3; i >= 0; i--)
+            if (c + (uint32_t)i < nch && E[i] > e) first = (uint32_t)i;
+        const uint64_t m = ballot(first < 4);
+        if (m) {
+            const int l = __builtin_ctzll(m);
+            const uint32_t f = rdlane(first, l);
+            bc = b + 4u * (uint32_t)l + f;
+            // walk position before chunk bc: the previous chunk's end (same or previous lane)
+            const uint32_t prev = f == 0 ? 0u : f == 1 ? E[0] : f == 2 ? E[1] : E[2];
+            const uint32_t prev_lane = dpp<0x138, 0xf>(E[3]);   // wave_shr:1
+            const uint32_t pv = rdlane(f ? prev : prev_lane, l);
+            before = bc == 0 ? rpos : (f == 0 && l == 0 ? before : pv);
+            break;
+        }
+        before = rdlane(E[3], WAVE - 1);   // chunk b + 4*64 - 1 ends here (all <= e)
+    }
+    // the break op inside chunk bc: lanes 0-7 take its ops
+    const uint32_t w = ln < CHUNK ? P.cigar[op0 + (uint64_t)bc * CHUNK + (uint32_t)ln] : 0u;
+    const uint32_t after = before + wave_scan_add(ln < CHUNK ? ref_adv(w) : 0u);
+    const uint64_t m = ballot(ln < CHUNK && after > e);
+    const int k = __builtin_ctzll(m);   // exists: the chunk ends past e
+    op_idx = bc * CHUNK + (uint32_t)k;
+    return rdlane(after, k);
+}
+
+template <int KIND, bool COUNT>
+__device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
+                                             WinStats &st) {
+    // Walk positions of index-walked reads are < 2^29 (the others are flagged slow at load
+    // time); windows ending at or past 2^31 take the exact per-read path.
+    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
+    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
+    int64_t lo, hi;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
+    const int ln = lane_id();
+    uint32_t live_ops = 0;   // COUNT builds
+    for (int64_t rb = lo; rb < hi; rb += WAVE) {
+        const int64_t r = rb + ln;
+        const bool inb = r < hi;
+        const uint4 rc = inb ? P.rec[r] : make_uint4(0, 0, 0, 0);
+        const uint4 r2 = inb ? P.rec2[r] : make_uint4(0, 0, 0, 0);
+        const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
+        const bool slow = (rc.z & SLOW_BIT) != 0;
+        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
+        const bool live = ovl && !slow && ncig > 0;
+        const uint32_t wend = r2.x;                                 // walk position after the last op
+        const bool brk = wend > e;                                  // refinement.c:145 fires somewhere
+        // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
+        if (KIND != K_INS) {
+            const bool z = ovl && ncig == 0 && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
+            if (KIND == K_START) sink.push(z && (clip & SVT_CLIP_LAST_S), (int32_t)rpos);       // :152
+            else sink.push(z && (clip & SVT_CLIP_FIRST_S), (int32_t)(rpos + 1u));                // :210-220
+        }
+        if (COUNT) {
+            st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
+            if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
+        }
+        // candidate ops processed before the break (refinement.c:124-136 / :190-200 / :299-310)
+        {
+            const uint2 *evp = P.ev + ((uint64_t)r2.w << 32 | r2.z);
+            uint32_t n = live ? r2.y : 0u;
+            uint2 a = n > 0 ? evp[0] : make_uint2(0, 0), b = n > 1 ? evp[1] : make_uint2(0, 0);
+            for (uint32_t k = 0; ballot(k < n); k += 2) {
+                if (k < n) {
+                    if (a.x > e) n = k;
+                    else if (is_candidate_op<KIND>(a.y & 0xfu, a.y >> 4))
+                        sink.push1(KIND == K_END ? (int32_t)(a.x + (a.y >> 4) + 1u) : (int32_t)a.x);
+                }
+                if (k + 1 < n) {
+                    if (b.x > e) n = k + 1;
+                    else if (is_candidate_op<KIND>(b.y & 0xfu, b.y >> 4))
+                        sink.push1(KIND == K_END ? (int32_t)(b.x + (b.y >> 4) + 1u) : (int32_t)b.x);
+                }
+                a = k + 2 < n ? evp[k + 2] : make_uint2(0, 0);
+                b = k + 3 < n ? evp[k + 3] : make_uint2(0, 0);
+            }
+        }
+        // soft-clip candidates at the walk's stop
+        if (KIND == K_START)   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
+            sink.push(live && !brk && (clip & SVT_CLIP_LAST_S) && s <= wend, (int32_t)wend);
+        if (KIND == K_END) {   // leading S, s <= pos <= e: walked rp + 1  (refinement.c:210-220)
+            const bool stop = live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
+            sink.push(stop && !brk, (int32_t)(wend + 1u));
+            uint64_t m = COUNT ? 0ull : ballot(stop && brk);
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                uint32_t bi;
+                const uint32_t aft = break_after(P, P.off64[rb + l], rdlane(ncig, l), rdlane(rpos, l), e, bi);
+                if (ln == 0) sink.push1((int32_t)(aft + 1u));
+            }
+        }
+        if (COUNT) {   // ops walked: every op up to the break op, or all ops; + the soft-clip test word
+            uint64_t m = ballot(live);
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t nc = rdlane(ncig, l), rp = rdlane(rpos, l);
+                const bool bl = rdlane(wend, l) > e;
+                uint32_t walked = nc;
+                if (bl) {
+                    uint32_t bi;
+                    const uint32_t aft = break_after(P, P.off64[rb + l], nc, rp, e, bi);
+                    walked = bi + 1;
+                    if (KIND == K_END && (rdlane(clip, l) & SVT_CLIP_FIRST_S) && s <= rp && rp <= e && ln == 0)
+                        sink.push1((int32_t)(aft + 1u));
+                    if (KIND == K_START && bi + 1 != nc) walked++;   // cigar[n-1] test word
+                }
+                if (ln == 0) live_ops += walked;
+            }
+        }
+        // reads whose walk could leave the index's range: exact per-read replay
         uint64_t sm = ballot(ovl && slow);
         while (sm) {
             const int l = __builtin_ctzll(sm);
             sm &= sm - 1;
-            walk_read<KIND, COUNT>(P.cigar, S0 + (uint64_t)(int64_t)rdlane_i(st0, l), rdlane(ncig, l), rdlane(rpos, l),
-                                   rdlane(clip, l), s, e, sink, st);
+            walk_read<KIND, COUNT>(P.cigar, P.off64[rb + l], rdlane(ncig, l), rdlane(rpos, l), rdlane(clip, l), s, e,
+                                   sink, st);
         }
     }
-    if (nev) flush_chunks<KIND>(cg, L, nev, e, sink);
-    if (COUNT) st.ops += rdlane(wave_scan_add(live_ops), WAVE - 1);
+    if (COUNT) st.ops += rdlane(live_ops, 0);
 }
 
 // ------------------------------------------------------------------ sort + vote (A8-A10)
@@ -914,14 +1178,15 @@ struct WinLds {
     int32_t ncand;
 };
 
-constexpr int G_PERREAD = 0, G_STREAM = 1, G_INDEX = 2;   // window gather variants (SVTREK_GATHER)
+constexpr int G_PERREAD = 0, G_STREAM = 1, G_INDEX = 2, G_EVENT = 3;   // window gather variants (SVTREK_GATHER)
 
 template <int KIND, bool COUNT, int G>
 __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
                                           WinLds &L) {
     if (lane_id() == 0) *sink.cnt = 0;
     wave_sync();
-    if (G == G_INDEX) gather_index<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.il);
+    if (G == G_EVENT) gather_event<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    else if (G == G_INDEX) gather_index<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.il);
     else if (G == G_STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.sl);
     else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
     wave_sync();
@@ -969,16 +1234,27 @@ constexpr int WPB = 4;
 #define SVT_INTERLEAVE_WINDOWS 0
 #endif
 
-template <bool COUNT, int G>
+// The timed index-walk kernel is held to 64 VGPRs = 8 waves per SIMD (the CU's maximum):
+// the walk is bound by dependent-load latency, so resident waves are what hide it.
 #ifndef SVT_WAVES_PER_EU
-#define SVT_WAVES_PER_EU 0       // 0: let the compiler choose (70 VGPRs -> 7 waves/SIMD)
+#define SVT_WAVES_PER_EU 8
 #endif
 #if SVT_WAVES_PER_EU
 #define SVT_OCC __attribute__((amdgpu_waves_per_eu(SVT_WAVES_PER_EU, SVT_WAVES_PER_EU)))
 #else
 #define SVT_OCC
 #endif
-__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_kernel(KArgs a) {
+template <bool COUNT, int G>
+__device__ __forceinline__ void refine_body(const KArgs &a);
+
+template <bool COUNT, int G>
+__global__ __launch_bounds__(64 * WPB) void refine_kernel(KArgs a) { refine_body<COUNT, G>(a); }
+
+__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_index_kernel(KArgs a) { refine_body<false, G_INDEX>(a); }
+__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_event_kernel(KArgs a) { refine_body<false, G_EVENT>(a); }
+
+template <bool COUNT, int G>
+__device__ __forceinline__ void refine_body(const KArgs &a) {
     __shared__ WinLds lds_all[WPB];
     const uint32_t wid = threadIdx.x >> 6;
     const uint32_t g = blockIdx.x * WPB + wid;
@@ -1055,22 +1331,23 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 // svt_load_pileup's per-op work, on the device: one wave per read copies the read's
 // CIGAR words from the caller's unpadded layout into the padded arena (coalesced), and
 // builds the read's chunk index: for every CHUNK ops (zero padding up to ALIGN_OPS
-// included) the reference walk position after the chunk (refinement.c:141, a wave prefix
-// scan carried across 64-op steps) and the DEL/INS candidate flags.  Reads whose walk
-// reaches 2^30 (the chunk word's range) are flagged SLOW_BIT: those take walk_read's exact
-// uint32 replay.  The host only does per-read work (offsets, prefix-max, buckets).
+// included; a read with n_cigar == 0 still owns one padded lane group) the reference walk
+// position after the chunk (refinement.c:141, a wave prefix scan carried across 64-op
+// steps), the DEL/INS candidate flags and, on the read's first chunk, CH_HEAD.  Reads whose
+// walk reaches 2^29 (the chunk word's range) are flagged SLOW_BIT: those take walk_read's
+// exact uint32 replay.  The host only does per-read work (offsets, prefix-max, buckets).
 __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ raw, const uint64_t *__restrict__ raw_off,
                                                    const uint64_t *__restrict__ poff, uint4 *rec,
                                                    uint32_t *__restrict__ arena, uint32_t *__restrict__ chunk,
-                                                   int64_t nr) {
+                                                   uint4 *__restrict__ rec2, uint32_t *__restrict__ nev_out, int64_t nr) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= nr) return;
     const int ln = lane_id();
     const uint64_t o0 = raw_off[r], n = raw_off[r + 1] - o0, dst = poff[r];
-    const uint64_t npad = (n + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1);
+    const uint64_t npad = n ? (n + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1) : (uint64_t)ALIGN_OPS;
     const uint32_t rpos = rec[r].x;
     uint64_t walk = 0;
-    uint32_t carry = rpos;
+    uint32_t carry = rpos, nev = 0;
     for (uint64_t i0 = 0; i0 < npad; i0 += WAVE) {
         const uint64_t i = i0 + (uint64_t)ln;
         const uint32_t w = i < n ? raw[o0 + i] : 0u;
@@ -1083,13 +1360,51 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
         if ((ln & (CHUNK - 1)) == CHUNK - 1 && i < npad) {
             const int sh = ln & ~(CHUNK - 1);
             chunk[(dst + i0) / CHUNK + (uint64_t)(ln / CHUNK)] =
-                (after & CH_POS) | (((dm >> sh) & 0xffull) ? CH_DEL : 0u) | (((im >> sh) & 0xffull) ? CH_INS : 0u);
+                (after & CH_POS) | (i0 == 0 && sh == 0 ? CH_HEAD : 0u) | (((dm >> sh) & 0xffull) ? CH_DEL : 0u) |
+                (((im >> sh) & 0xffull) ? CH_INS : 0u);
         }
         carry = rdlane(after, WAVE - 1);
+        nev += (uint32_t)__popcll(dm | im);
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) walk += __shfl_xor(walk, d, WAVE);
-    if (ln == 0 && (uint64_t)rpos + walk >= INDEX_LIMIT) rec[r].z |= SLOW_BIT;
+    if (ln == 0) {
+        if ((uint64_t)rpos + walk >= INDEX_LIMIT) rec[r].z |= SLOW_BIT;
+        rec2[r] = make_uint4(rpos + (uint32_t)walk, nev, 0u, 0u);
+        nev_out[r] = nev;
+    }
+}
+
+// Second load pass: every read's candidate ops (D > 50 or I >= 50, refinement.c:124,:190,:299)
+// with the walk position before each (refinement.c:141), in op order, at the read's event
+// offset (an exclusive scan of pack_kernel's counts).
+__global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__ arena, const uint64_t *__restrict__ poff,
+                                                    const uint4 *__restrict__ rec, uint4 *__restrict__ rec2,
+                                                    const uint64_t *__restrict__ evoff, uint2 *__restrict__ ev,
+                                                    int64_t nr) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nr) return;
+    const int ln = lane_id();
+    const uint4 rc = rec[r];
+    const uint64_t n = rc.z & NCIG_MASK, src = poff[r], o0 = evoff[r];
+    if (ln == 0) rec2[r].z = (uint32_t)o0, rec2[r].w = (uint32_t)(o0 >> 32);
+    if (evoff[r + 1] == o0) return;
+    uint32_t carry = rc.x;
+    uint64_t k = o0;
+    for (uint64_t i0 = 0; i0 < n; i0 += WAVE) {
+        const uint64_t i = i0 + (uint64_t)ln;
+        const uint32_t w = i < n ? arena[src + i] : 0u;
+        const uint32_t adv = ref_adv(w);
+        const uint32_t after = carry + wave_scan_add(adv);
+        const bool c = is_candidate_op<K_START>(w & 0xfu, w >> 4) || is_candidate_op<K_INS>(w & 0xfu, w >> 4);
+        const uint64_t m = ballot(c);
+        if (c) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            ev[k + rank] = make_uint2(after - adv, w);
+        }
+        k += (uint64_t)__popcll(m);
+        carry = rdlane(after, WAVE - 1);
+    }
 }
 
 }  // namespace
@@ -1098,19 +1413,21 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
 struct svt_ctx {
     svt_params prm{};
     int device = 0;
-    int gather = G_INDEX;         // SVTREK_GATHER=stream / perread select the A/B variants
+    int gather = G_EVENT;         // SVTREK_GATHER=index / stream / perread select the A/B variants
     char err[512] = {0};
     // pileup
     int32_t n_targets = 0;
     int64_t n_reads = 0;
     uint64_t n_ops = 0;
-    int32_t *d_pos = nullptr, *d_emax = nullptr, *d_maxspan = nullptr;
+    int32_t *d_pos = nullptr, *d_emax = nullptr;
     uint4 *d_rec = nullptr;
     uint64_t *d_off64 = nullptr;
     int64_t *d_tid_off = nullptr, *d_bkt_off = nullptr;
-    uint32_t *d_bkt = nullptr;
+    uint2 *d_bkt = nullptr;
     uint32_t *d_cigar = nullptr;
     uint32_t *d_chunk = nullptr;
+    uint4 *d_rec2 = nullptr;
+    uint2 *d_ev = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
     // batch scratch
@@ -1143,15 +1460,16 @@ void hfree(T *&p) {
 }
 
 void free_pileup(svt_ctx *c) {
-    hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_maxspan); hfree(c->d_rec); hfree(c->d_off64);
+    hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar); hfree(c->d_chunk);
+    hfree(c->d_rec2); hfree(c->d_ev);
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
-                       c->d_maxspan, c->d_cigar, c->d_chunk, c->n_targets};
+                       c->d_cigar, c->d_chunk, c->d_rec2, c->d_ev, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
                     c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
     a.loci = d_loci;
@@ -1173,9 +1491,12 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 64, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
-    if (c->gather == G_INDEX) {
+    if (c->gather == G_EVENT) {
+        if (count) hipLaunchKernelGGL((refine_kernel<true, G_EVENT>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL(refine_event_kernel, grid, block, 0, st, a);
+    } else if (c->gather == G_INDEX) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_INDEX>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((refine_kernel<false, G_INDEX>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL(refine_index_kernel, grid, block, 0, st, a);
     } else if (c->gather == G_STREAM) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_STREAM>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((refine_kernel<false, G_STREAM>), grid, block, 0, st, a);
@@ -1223,7 +1544,11 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     if (!c) return SVT_ENOMEM;
     c->prm = *params;
     const char *g = getenv("SVTREK_GATHER");
-    c->gather = !g ? G_INDEX : strcmp(g, "perread") == 0 ? G_PERREAD : strcmp(g, "stream") == 0 ? G_STREAM : G_INDEX;
+    c->gather = !g ? G_EVENT
+                : strcmp(g, "perread") == 0 ? G_PERREAD
+                : strcmp(g, "stream") == 0  ? G_STREAM
+                : strcmp(g, "index") == 0   ? G_INDEX
+                                            : G_EVENT;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;
@@ -1263,16 +1588,16 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     const uint64_t nops = nr > 0 ? p->cig_off[nr] : 0;
     if (nr > 0 && p->cig_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "cig_off[0] != 0");
 
-    std::vector<int32_t> emax((size_t)nr), maxspan((size_t)(nt > 0 ? nt : 1), 0);
+    std::vector<int32_t> emax((size_t)nr);
     std::vector<uint4> rec((size_t)nr);
     std::vector<uint64_t> poff((size_t)nr + 1, 0);   // padded CIGAR offsets (multiples of ALIGN_OPS)
     std::vector<int64_t> bkt_off((size_t)nt + 1, 0);
-    std::vector<uint32_t> bkt;
+    std::vector<uint2> bkt;
     uint64_t pw = 0;
     for (int32_t t = 0; t < nt; t++) {
         const int64_t r0 = p->tid_off[t], r1 = p->tid_off[t + 1];
         if (r1 - r0 > 0xffffffffll) return fail(c, SVT_EINVAL, "pileup: %s", "> 2^32 reads on one contig");
-        int32_t m = INT32_MIN, ms = 0, maxpos = 0;
+        int32_t m = INT32_MIN, maxpos = 0;
         for (int64_t r = r0; r < r1; r++) {
             if (r > r0 && p->pos[r] < p->pos[r - 1])
                 return fail(c, SVT_EINVAL, "pileup: %s", "reads not sorted by pos within a contig");
@@ -1287,24 +1612,27 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
                                 ((p->cigar[o0] & 0xfu) == OP_SOFT ? 2u : 0u)) : 0u;
             // SLOW_BIT (walk reaching 2^30) is set by pack_kernel on the device
             if (p->endpos[r] > m) m = p->endpos[r];
-            if (p->endpos[r] - p->pos[r] > ms) ms = p->endpos[r] - p->pos[r];
             maxpos = std::max(maxpos, p->pos[r]);
             emax[(size_t)r] = m;
             poff[(size_t)r] = pw;
             rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | (clip << 30),
                                         (uint32_t)pw);
-            pw += ((uint64_t)ncig + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1);
+            // every read, n_cigar == 0 included, owns >= 1 lane group (its head chunk)
+            pw += std::max<uint64_t>(((uint64_t)ncig + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1), ALIGN_OPS);
         }
         if (r1 > r0 && pw - poff[(size_t)r0] >= (1ull << 31))
             return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^31 CIGAR ops on one contig");
-        maxspan[(size_t)t] = ms;
-        // bucket b: first contig-relative read with pos >= b << BKT_SHIFT, b = 0..nb-1
-        const int64_t nb = (r1 > r0 ? ((int64_t)maxpos >> BKT_SHIFT) + 2 : 1) + 1;
+        // bucket b = 0..nb-1: {first contig-relative read with pos >= b << BKT_SHIFT, first with
+        // emax >= b << BKT_SHIFT}; the last bucket lies past every pos and endpos: {nr, nr}
+        const int64_t top = r1 > r0 ? std::max<int64_t>(maxpos, m) : 0;
+        const int64_t nb = (top >> BKT_SHIFT) + 2;
         bkt_off[(size_t)t] = (int64_t)bkt.size();
-        int64_t r = r0;
+        int64_t rp = r0, re = r0;
         for (int64_t b = 0; b < nb; b++) {
-            while (r < r1 && ((int64_t)p->pos[r] >> BKT_SHIFT) < b) r++;
-            bkt.push_back((uint32_t)(r - r0));
+            const int64_t x = b << BKT_SHIFT;
+            while (rp < r1 && (int64_t)p->pos[rp] < x) rp++;
+            while (re < r1 && (int64_t)emax[(size_t)re] < x) re++;
+            bkt.push_back(make_uint2((uint32_t)(rp - r0), (uint32_t)(re - r0)));
         }
     }
     poff[(size_t)nr] = pw;
@@ -1314,7 +1642,6 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
     if ((s = upload(c, c->d_rec, rec.data(), (size_t)nr))) return s;
     if ((s = upload(c, c->d_off64, poff.data(), poff.size()))) return s;
-    if ((s = upload(c, c->d_maxspan, maxspan.data(), maxspan.size()))) return s;
     if ((s = upload(c, c->d_bkt, bkt.data(), bkt.size()))) return s;
     if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
     if (nt > 0) { if ((s = upload(c, c->d_tid_off, p->tid_off, (size_t)nt + 1))) return s; }
@@ -1324,22 +1651,45 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     // words together with the chunk index (one word per CHUNK arena words)
     if ((s = upload<uint32_t>(c, c->d_cigar, nullptr, 0, (size_t)pw + CIGAR_PAD))) return s;
     if ((s = upload<uint32_t>(c, c->d_chunk, nullptr, 0, (size_t)(pw / CHUNK) + CHUNK_PAD))) return s;
+    if ((s = upload<uint4>(c, c->d_rec2, nullptr, 0, (size_t)std::max<int64_t>(nr, 1)))) return s;
     if (nr > 0) {
-        uint32_t *d_raw = nullptr;
-        uint64_t *d_raw_off = nullptr;
+        // pass 1 (pack_kernel): padded arena, chunk index, walk ends, candidate-op counts;
+        // host: exclusive scan of the counts; pass 2 (event_kernel): the candidate-op lists
+        uint32_t *d_raw = nullptr, *d_nev = nullptr;
+        uint64_t *d_raw_off = nullptr, *d_evoff = nullptr;
+        std::vector<uint32_t> nev((size_t)nr);
+        std::vector<uint64_t> evoff((size_t)nr + 1, 0);
         hipError_t e = hipMalloc(&d_raw, std::max<uint64_t>(nops, 1) * 4);
         if (e == hipSuccess) e = hipMalloc(&d_raw_off, ((size_t)nr + 1) * 8);
+        if (e == hipSuccess) e = hipMalloc(&d_nev, (size_t)nr * 4);
+        if (e == hipSuccess) e = hipMalloc(&d_evoff, ((size_t)nr + 1) * 8);
         if (e == hipSuccess && nops) e = hipMemcpy(d_raw, p->cigar, nops * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, d_raw, d_raw_off,
-                               c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, (int64_t)nr);
+                               c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, c->d_rec2, d_nev, (int64_t)nr);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpy(nev.data(), d_nev, (size_t)nr * 4, hipMemcpyDeviceToHost);
+        hfree(d_raw);
+        hfree(d_raw_off);
+        hfree(d_nev);
+        if (e == hipSuccess) {
+            for (int64_t r = 0; r < nr; r++) evoff[(size_t)r + 1] = evoff[(size_t)r] + nev[(size_t)r];
+            e = hipMemcpy(d_evoff, evoff.data(), ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
+        }
+        if (e == hipSuccess) e = hipMalloc(&c->d_ev, std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2));
+        if (e == hipSuccess) {
+            c->dev_bytes += std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2);
+            hipLaunchKernelGGL(event_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
+                               c->d_off64, c->d_rec, c->d_rec2, d_evoff, c->d_ev, (int64_t)nr);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipDeviceSynchronize();
-        hfree(d_raw);
-        hfree(d_raw_off);
+        hfree(d_evoff);
         if (e != hipSuccess) return fail(c, SVT_EDEVICE, "pileup pack: %s", hipGetErrorString(e));
+    } else if ((s = upload<uint2>(c, c->d_ev, nullptr, 0, 1))) {
+        return s;
     }
     c->n_targets = nt;
     c->n_reads = nr;
@@ -1455,7 +1805,8 @@ svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, i
             a.sw_sub = d_sub;
             a.sw_out = d_res;
             const dim3 grid((unsigned)((ns + WPB - 1) / WPB)), block(64 * WPB);
-            if (c->gather == G_INDEX) hipLaunchKernelGGL(sw_kernel<G_INDEX>, grid, block, 0, nullptr, a);
+            if (c->gather == G_EVENT) hipLaunchKernelGGL(sw_kernel<G_EVENT>, grid, block, 0, nullptr, a);
+            else if (c->gather == G_INDEX) hipLaunchKernelGGL(sw_kernel<G_INDEX>, grid, block, 0, nullptr, a);
             else if (c->gather == G_STREAM) hipLaunchKernelGGL(sw_kernel<G_STREAM>, grid, block, 0, nullptr, a);
             else hipLaunchKernelGGL(sw_kernel<G_PERREAD>, grid, block, 0, nullptr, a);
             chk(hipGetLastError(), "sw_kernel: %s");

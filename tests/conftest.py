@@ -28,8 +28,8 @@ def engine_factory():
 
     engines = []
 
-    def make(params=None, gather="index"):
-        """gather: "index" (chunk-index walk, default), "stream" (full CIGAR stream) or
+    def make(params=None, gather="event"):
+        """gather: "event" (candidate-op lists, default), "index" (chunk-index walk), "stream" (full CIGAR stream) or
         "perread" (per-read walk) -- the SVTREK_GATHER variants of the engine."""
         old = os.environ.get("SVTREK_GATHER")
         os.environ["SVTREK_GATHER"] = gather

@@ -21,6 +21,6 @@ tail -5 "$OUT/pytest.log"
 if [ $rc -gt 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
 run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
 tail -1 "$OUT/bench.log"
-SVTREK_GATHER=stream run bench_streamvar 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
+SVTREK_GATHER=index run bench_streamvar 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
 tail -1 "$OUT/bench_streamvar.log"
 exit $rc
