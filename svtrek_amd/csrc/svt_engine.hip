@@ -566,7 +566,8 @@ __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141:
 #define SVT_QSCAN 0              // 1: queue slots from a wave prefix scan instead of LDS atomics
 #endif
 #ifndef SVT_DIAG
-#define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 2 = no chunk resolve
+#define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 2 = no chunk
+                                 // resolve (index walk), 3 = no refine_end stop search (event walk), 4 = no vote
 #endif
 // LEAN: the mid-tile overflow flush (rare), which must leave the walk's registers alone:
 // one 16-B half of the chunk in flight at a time.
@@ -912,6 +913,9 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
     if (!read_range(P, tid, beg, end, lo, hi)) return;
+#if SVT_DIAG == 1
+    if (lo < hi) return;     // diagnostic build: region query only
+#endif
     const int ln = lane_id();
     uint32_t live_ops = 0;   // COUNT builds
     for (int64_t rb = lo; rb < hi; rb += WAVE) {
@@ -961,7 +965,7 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
         if (KIND == K_END) {   // leading S, s <= pos <= e: walked rp + 1  (refinement.c:210-220)
             const bool stop = live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
             sink.push(stop && !brk, (int32_t)(wend + 1u));
-            uint64_t m = COUNT ? 0ull : ballot(stop && brk);
+            uint64_t m = COUNT || SVT_DIAG == 3 ? 0ull : ballot(stop && brk);
             while (m) {
                 const int l = __builtin_ctzll(m);
                 m &= m - 1;
@@ -1043,6 +1047,20 @@ __device__ __forceinline__ int32_t mean_round(int64_t tot, int32_t cnt) {
     return (int32_t)(uint32_t)(t / (uint64_t)(int64_t)cnt);
 }
 
+// mean_round of a cluster whose smallest value is `base`.  With base >= 0 every value is
+// >= 0, the reference's uint64 total is the exact sum, and (sum + cnt/2) / cnt =
+// base + (sum - cnt*base + cnt/2) / cnt: a 32-bit division whenever the offsets' sum fits.
+__device__ __forceinline__ int32_t mean_cluster(int64_t tot, int32_t cnt, int32_t base) {
+    if (base >= 0) {
+        const int64_t d = tot - (int64_t)cnt * (int64_t)base;
+        if (d < (int64_t)0x7fffffff) {
+            const uint32_t q = ((uint32_t)d + (uint32_t)(cnt / 2)) / (uint32_t)cnt;
+            return (int32_t)((uint32_t)base + q);
+        }
+    }
+    return mean_round(tot, cnt);
+}
+
 // consensus_pos (refinement.c:41-101) on sorted A[0..n) with prefix sums P[0..n].
 __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t pos, const KParams &k) {
     const int ln = lane_id();
@@ -1069,7 +1087,7 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
             int32_t a = A[i];
             int32_t kk = first_geq(A, 0, i, (int64_t)a - ci);   // contiguous j<i with a <= A[j]+ci
             cnt = i - kk + 1;
-            cand = mean_round(P[i + 1] - P[kk], cnt);
+            cand = mean_cluster(P[i + 1] - P[kk], cnt, A[kk]);
         }
         for (int l = 0; l < lim; l++) {
             int32_t c = rdlane_i(cnt, l), v = rdlane_i(cand, l);
@@ -1094,7 +1112,7 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
             int32_t a = A[i];
             int32_t m = first_greater(A, i + 1, n, (int64_t)a + ci);   // contiguous j>i with A[j] <= a+ci
             cnt = m - i;
-            cand = mean_round(P[m] - P[i], cnt);
+            cand = mean_cluster(P[m] - P[i], cnt, a);
         }
         for (int l = 0; l < lim; l++) {
             int32_t c = rdlane_i(cnt, l), v = rdlane_i(cand, l);
@@ -1149,11 +1167,27 @@ template <int VOTE>
 __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
                                                  int32_t &support) {
     const int ln = lane_id();
-    int N = 1;
-    while (N < n) N <<= 1;
-    for (int i = n + ln; i < N; i += WAVE) buf[i] = INT32_MAX;
-    wave_sync();
-    wave_bitonic_sort(buf, N);
+    if (n <= WAVE) {
+        // one value per lane: bitonic network in registers (lane-xor exchanges), then one
+        // store of the sorted values
+        int32_t x = ln < n ? buf[ln] : INT32_MAX;
+#pragma unroll
+        for (int kk = 2; kk <= WAVE; kk <<= 1) {
+#pragma unroll
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                const int32_t y = __shfl_xor(x, j, WAVE);
+                x = (((ln & j) == 0) == ((ln & kk) == 0)) ? min(x, y) : max(x, y);
+            }
+        }
+        wave_sync();
+        buf[ln] = x;
+    } else {
+        int N = 1;
+        while (N < n) N <<= 1;
+        for (int i = n + ln; i < N; i += WAVE) buf[i] = INT32_MAX;
+        wave_sync();
+        wave_bitonic_sort(buf, N);
+    }
     int64_t carry = 0;
     if (ln == 0) P[0] = 0;
     for (int32_t b = 0; b < n; b += WAVE) {
@@ -1204,6 +1238,7 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     }
     support = 0;
     if (n < a.prm.min_count) return -1;                    // refinement.c:43-45 (sliding: no support >= min_count)
+    if (SVT_DIAG == 4) return n;   // diagnostic build: no sort/vote
     if (n <= CAP) return sort_and_vote<VOTE>(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm, support);
     // spill: a slab for N ints + (n+1) int64 from the device pool, then re-gather into it
     if (COUNT && lane_id() == 0) wk[4] += 1;
