@@ -9,12 +9,15 @@ N>1: every rank owns its own shard (independent loci, no data-path collective: w
 scaling); each step ends with the one RCCL gather of refined calls to rank 0 that the
 multi-GPU path performs.  Rank 0 prints ONE JSON line.
 
-roofline: algorithmic bytes of the dominant kernel (refine_kernel) per launch =
+roofline: algorithmic bytes of the timed kernel (refine_event_kernel) per launch =
   16 B/locus in + 8 B/locus out + Σ_windows Σ_yielded reads (12 B + 4 B × CIGAR words walked)
-(counted exactly by svt_count_work) ÷ the kernel's mean duration,
-measured with HIP events on the launch stream.  cpu_baseline: the CPU oracle
-(restatement of the reference's tpool path over the same in-memory pileup) timed on
-rank 0's host cores on the same workload.
+(what the reference's walk touches; counted exactly by svt_count_work) ÷ the
+kernel's mean duration, measured with HIP events on the launch stream.  The event walk reads
+per-read summaries built once by svt_load_pileup (candidate-op lists, walk ends, chunk index)
+instead of every CIGAR word, so `achieved` can exceed the HBM peak; `traffic` (measured HBM
+bytes per launch, rocprofv3 PMC, profiles/traffic.json) and `traffic_frac` give the kernel's
+physical bandwidth.  cpu_baseline: the CPU oracle (restatement of the reference's tpool path
+over the same in-memory pileup) timed on rank 0's host cores on the same workload.
 """
 from __future__ import annotations
 
@@ -178,14 +181,16 @@ def main() -> int:
     alg_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
     achieved = alg_bytes / (kern_mean_ms * 1e-3) / 1e9
 
-    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes, when they
-    # were taken on this engine version and workload (tools/gpu_profile.sh -> profiles/traffic.json)
+    # HBM traffic of the timed kernel from the committed rocprofv3 PMC passes, when they were
+    # taken on this engine version, workload and kernel (tools/gpu_profile.sh -> profiles/traffic.json)
+    gather = os.environ.get("SVTREK_GATHER", "event")
+    kernel = {"event": "refine_event_kernel", "index": "refine_index_kernel"}.get(gather, "refine_kernel")
     traffic = traffic_src = None
     try:
-        _ver = _engine_version
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
-        if tj.get("engine_version") == _ver() and tj.get("workload") == args.workload:
+        if (tj.get("engine_version") == _engine_version() and tj.get("workload") == args.workload
+                and tj.get("kernel") == kernel and args.replicate == 1):
             traffic, traffic_src = int(tj["hbm_bytes_per_launch"]), tj.get("source")
     except (OSError, ValueError, KeyError):
         pass
@@ -220,9 +225,14 @@ def main() -> int:
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_gbs": round(traffic / (kern_mean_ms * 1e-3) / 1e9, 2) if traffic else None,
+                         "traffic_frac": round(traffic / (kern_mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                         if traffic else None,
                          "traffic_source": traffic_src,
-                         "kernel": "refine_kernel", "kernel_ms_mean": round(kern_mean_ms, 5),
-                         "kernel_ms_min": round(kern_ms[0], 5), "alg_bytes_per_launch": alg_bytes},
+                         "kernel": kernel, "gather": gather, "kernel_ms_mean": round(kern_mean_ms, 5),
+                         "kernel_ms_min": round(kern_ms[0], 5), "alg_bytes_per_launch": alg_bytes,
+                         "note": "achieved = the reference walk's bytes (SURVEY 8(d)) / kernel time; the event walk "
+                                 "reads load-time per-read summaries instead of every CIGAR word, so achieved can "
+                                 "exceed peak; traffic = measured HBM bytes per launch" if gather == "event" else None},
             "cpu_baseline": cpu,
             "work": work,
             "setup_s": {"generate": round(gen_s, 2), "load_pileup": round(load_s, 2)},

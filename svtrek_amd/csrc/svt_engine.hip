@@ -89,8 +89,9 @@ struct KArgs {
     svt_result *out;
     uint32_t n;                 // loci
     int32_t *pool;              // spill slabs (int32 words)
-    unsigned long long *pool_head;
+    unsigned long long *pool_head;   // epoch << 40 | words handed out in that launch
     unsigned long long pool_words;
+    uint32_t epoch;                  // this launch's pool epoch (1 .. 2^24-1)
     int32_t *status;            // bit0: spill pool exhausted
     unsigned long long *work;   // svt_work counters (COUNT builds only)
     const uint4 *sw_sub;        // sliding_window_ins mode: per sub-window {chrom, start, end, 0}
@@ -904,6 +905,63 @@ __device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0
     return rdlane(after, k);
 }
 
+// Row-parallel form of break_after for refine_end's soft-clip stops: up to 4 breaking reads
+// at once, one 16-lane row each (DPP row shifts never cross a row).  Lanes of row g take
+// read `l` = the g-th set bit of `m` (block lane), consume those bits, and push after + 1.
+__device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, int64_t rb, uint64_t m, uint32_t ncig_v,
+                                              uint32_t rpos_v, uint32_t e, Sink &sink) {
+    const int ln = lane_id(), g = ln >> 4, t = ln & 15;
+    int my = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (!m) break;
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        if (g == q) my = l;
+    }
+    const bool has = my >= 0;
+    // per-row read parameters (a bpermute from the read's block lane)
+    const uint32_t ncig = (uint32_t)__shfl((int)ncig_v, has ? my : 0, WAVE);
+    const uint32_t rpos = (uint32_t)__shfl((int)rpos_v, has ? my : 0, WAVE);
+    const uint64_t op0 = has ? P.off64[rb + my] : 0ull;
+    const uint64_t c0 = op0 / CHUNK;
+    const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
+    bool found = false;
+    uint32_t bc = 0;
+    for (uint32_t it = 0;; it += 64) {   // 64 chunks (16 lanes x 4) per row per step
+        const uint32_t c = it + 4u * (uint32_t)t;
+        const bool act = has && !found && c < nch;
+        const uint4 q = act ? *reinterpret_cast<const uint4 *>(P.chunk + c0 + c) : make_uint4(0, 0, 0, 0);
+        const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
+        uint32_t first = 4;
+#pragma unroll
+        for (int i = 3; i >= 0; i--)
+            if (act && c + (uint32_t)i < nch && E[i] > e) first = (uint32_t)i;
+        const uint32_t rm = (uint32_t)(ballot(first < 4) >> (16 * g)) & 0xffffu;
+        const int lr = rm ? __builtin_ctz(rm) : 0;
+        const uint32_t f = (uint32_t)__shfl((int)first, 16 * g + lr, WAVE);
+        if (has && !found && rm) {
+            bc = it + 4u * (uint32_t)lr + f;
+            found = true;
+        }
+        if (!ballot(has && !found && it + 64 < nch)) break;
+    }
+    // the break chunk's ops (row lanes 0-7) and the walk position before it (row lane 8)
+    const uint32_t w = has && t < CHUNK ? P.cigar[op0 + (uint64_t)bc * CHUNK + (uint32_t)t] : 0u;
+    const uint32_t pv = has && t == CHUNK ? (bc ? P.chunk[c0 + bc - 1] & CH_POS : rpos) : 0u;
+    const uint32_t before = (uint32_t)__shfl((int)pv, 16 * g + CHUNK, WAVE);
+    uint32_t x = t < CHUNK ? ref_adv(w) : 0u;
+    x += dpp<0x111, 0xf>(x);   // inclusive row scan
+    x += dpp<0x112, 0xf>(x);
+    x += dpp<0x114, 0xf>(x);
+    x += dpp<0x118, 0xf>(x);
+    const uint32_t after = before + x;
+    const uint32_t bm = (uint32_t)(ballot(t < CHUNK && after > e) >> (16 * g)) & 0xffu;   // break op exists
+    const uint32_t a = (uint32_t)__shfl((int)after, 16 * g + (bm ? __builtin_ctz(bm) : 0), WAVE);
+    if (has && t == 0) sink.push1((int32_t)(a + 1u));   // refinement.c:210-220
+    return m;
+}
+
 template <int KIND, bool COUNT>
 __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
                                              WinStats &st) {
@@ -966,13 +1024,7 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
             const bool stop = live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
             sink.push(stop && !brk, (int32_t)(wend + 1u));
             uint64_t m = COUNT || SVT_DIAG == 3 ? 0ull : ballot(stop && brk);
-            while (m) {
-                const int l = __builtin_ctzll(m);
-                m &= m - 1;
-                uint32_t bi;
-                const uint32_t aft = break_after(P, P.off64[rb + l], rdlane(ncig, l), rdlane(rpos, l), e, bi);
-                if (ln == 0) sink.push1((int32_t)(aft + 1u));
-            }
+            while (m) m = stop_rows(P, rb, m, ncig, rpos, e, sink);
         }
         if (COUNT) {   // ops walked: every op up to the break op, or all ops; + the soft-clip test word
             uint64_t m = ballot(live);
@@ -1089,13 +1141,15 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
             cnt = i - kk + 1;
             cand = mean_cluster(P[i + 1] - P[kk], cnt, A[kk]);
         }
-        for (int l = 0; l < lim; l++) {
-            int32_t c = rdlane_i(cnt, l), v = rdlane_i(cand, l);
-            if (c > maxL) {
-                int32_t d = ref_abs(pos - v);
-                if (d < ci) return v;                    // early return, refinement.c:69-70
-                if (d < distL) { maxL = c; valL = v; distL = d; }
-            }
+        // the greedy accept in pass order, visiting only elements whose count beats maxL
+        const int32_t dd = ref_abs(pos - cand);
+        for (int l = -1;;) {
+            const uint64_t cm = ballot(ln < lim && ln > l && cnt > maxL);
+            if (!cm) break;
+            l = __builtin_ctzll(cm);
+            const int32_t c = rdlane_i(cnt, l), v = rdlane_i(cand, l), d = rdlane_i(dd, l);
+            if (d < ci) return v;                        // early return, refinement.c:67-68
+            if (d < distL) { maxL = c; valL = v; distL = d; }
         }
         if (stop) break;
     }
@@ -1114,13 +1168,14 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
             cnt = m - i;
             cand = mean_cluster(P[m] - P[i], cnt, a);
         }
-        for (int l = 0; l < lim; l++) {
-            int32_t c = rdlane_i(cnt, l), v = rdlane_i(cand, l);
-            if (c > maxR) {
-                int32_t d = ref_abs(pos - v);
-                if (d < ci) return v;
-                if (d < distR) { maxR = c; valR = v; distR = d; }
-            }
+        const int32_t dd = ref_abs(pos - cand);
+        for (int l = -1;;) {
+            const uint64_t cm = ballot(ln < lim && ln > l && cnt > maxR);
+            if (!cm) break;
+            l = __builtin_ctzll(cm);
+            const int32_t c = rdlane_i(cnt, l), v = rdlane_i(cand, l), d = rdlane_i(dd, l);
+            if (d < ci) return v;                        // refinement.c:88-89
+            if (d < distR) { maxR = c; valR = v; distR = d; }
         }
         if (stop) break;
     }
@@ -1245,8 +1300,17 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     int N = 1;
     while (N < n) N <<= 1;
     unsigned long long words = (unsigned long long)N + 2ull * (unsigned long long)(n + 2);
+    // the pool restarts for every launch: a head word tagged with another launch's epoch
+    // counts as empty (no per-launch reset on the host)
     unsigned long long base = 0;
-    if (lane_id() == 0) base = atomicAdd(a.pool_head, words);
+    if (lane_id() == 0) {
+        unsigned long long old = __hip_atomic_load(a.pool_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), seen;
+        do {
+            seen = old;
+            base = (uint32_t)(seen >> 40) == a.epoch ? (seen & ((1ull << 40) - 1ull)) : 0ull;
+            old = atomicCAS(a.pool_head, seen, ((unsigned long long)a.epoch << 40) | (base + words));
+        } while (old != seen);
+    }
     base = rdlane64(base, 0);
     if (base + words > a.pool_words) {
         if (lane_id() == 0) atomicOr(a.status, 1);
@@ -1472,7 +1536,8 @@ struct svt_ctx {
     // spill pool + status + work counters
     int32_t *d_pool = nullptr;
     unsigned long long pool_words = 0;
-    unsigned char *d_ctl = nullptr;   // [0,8) pool head, [8,12) status, [16,56) work
+    unsigned char *d_ctl = nullptr;   // [0,8) pool head (epoch-tagged), [8,12) sticky status, [16,56) work
+    uint32_t epoch = 0;               // launches so far (pool epochs cycle through 1 .. 2^24-1)
 };
 
 namespace {
@@ -1513,6 +1578,7 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
     a.pool = c->d_pool;
     a.pool_head = (unsigned long long *)c->d_ctl;
     a.pool_words = c->pool_words;
+    a.epoch = c->epoch;
     a.status = (int32_t *)(c->d_ctl + 8);
     a.work = count ? (unsigned long long *)(c->d_ctl + 16) : nullptr;
     a.sw_sub = nullptr;
@@ -1523,7 +1589,11 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
 svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t n, hipStream_t st, bool count) {
     if (n == 0) return SVT_OK;
     if (n > 0x3fffffffull) return fail(c, SVT_EINVAL, "batch too large (%s)", "n > 2^30-1");
-    HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 64, st));
+    // no per-launch reset of the spill pool (epoch-tagged head); the work counters of a
+    // counting launch start from zero; the head word is cleared once per epoch cycle
+    c->epoch = c->epoch % ((1u << 24) - 1u) + 1u;
+    if (c->epoch == 1) HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 8, st));
+    if (count) HIP_TRY(c, hipMemsetAsync(c->d_ctl + 16, 0, 48, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
     if (c->gather == G_EVENT) {
@@ -1745,7 +1815,10 @@ svt_status svt_sync(svt_ctx *c, void *stream) {
     HIP_TRY(c, hipStreamSynchronize((hipStream_t)stream));
     int32_t status = 0;
     HIP_TRY(c, hipMemcpy(&status, c->d_ctl + 8, 4, hipMemcpyDeviceToHost));
-    if (status & 1) return fail(c, SVT_EOVERFLOW, "%s", "candidate spill pool exhausted (raise spill_bytes)");
+    if (status & 1) {
+        HIP_TRY(c, hipMemset(c->d_ctl + 8, 0, 4));   // sticky until reported
+        return fail(c, SVT_EOVERFLOW, "%s", "candidate spill pool exhausted (raise spill_bytes)");
+    }
     return SVT_OK;
 }
 

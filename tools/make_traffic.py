@@ -1,12 +1,14 @@
 """Turn a tools/gpu_profile.sh run into the committed profile + profiles/traffic.json.
 
-    python tools/make_traffic.py gpurun_out/prof_TAG profiles/TAG [--workload cfg2_10kdel_30x_ont]
+    python tools/make_traffic.py gpurun_out/prof_TAG profiles/TAG [--workload W] [--kernel K]
 
 Copies the kernel stats / PMC CSVs and bench logs into profiles/TAG and writes
-profiles/traffic.json for the dominant kernel (refine_kernel<false, true>): HBM bytes per
-launch = 2 x FETCH_SIZE (gfx950 reports half the bytes of 16-B-per-lane streaming loads,
-MI355X_MICROARCH.md HBM section) + WRITE_SIZE, median over the profiled launches.  bench.py
-reports it as roofline.traffic when the engine version and workload match.
+profiles/traffic.json for the timed kernel (default refine_event_kernel): HBM bytes per launch =
+read bytes from the L2 fabric read requests by size class (TCC_EA0_RDREQ_{32B,64B,128B}:
+32/64/128 B each; cross-checked against 2 x FETCH_SIZE, which gfx950 tallies at 64 B per
+128-B request, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, median over the profiled
+launches.  bench.py reports it as roofline.traffic when engine version, workload and kernel
+match.
 """
 from __future__ import annotations
 
@@ -17,13 +19,17 @@ import os
 import shutil
 import statistics
 
-KERNEL = "refine_kernel<false, true>"
 
-
-def counter_values(path: str, name: str) -> list[float]:
+def counter_values(path: str, kernel: str, name: str) -> list[float]:
+    if not os.path.exists(path):
+        return []
     with open(path) as f:
         return [float(r["Counter_Value"]) for r in csv.DictReader(f)
-                if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == name]
+                if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
+
+
+def med(v: list[float]) -> float | None:
+    return statistics.median(v) if v else None
 
 
 def main() -> int:
@@ -31,40 +37,49 @@ def main() -> int:
     ap.add_argument("src")
     ap.add_argument("dst")
     ap.add_argument("--workload", default="cfg2_10kdel_30x_ont")
+    ap.add_argument("--kernel", default="refine_event_kernel")
     a = ap.parse_args()
     os.makedirs(a.dst, exist_ok=True)
     copies = {"trace/run_kernel_stats.csv": "kernel_stats.csv", "pmc_fetch/run_counter_collection.csv":
               "pmc_fetch_size.csv", "pmc_write/run_counter_collection.csv": "pmc_write_size.csv",
-              "trace.log": "bench_under_rocprof.log"}
+              "pmc_rdreq/run_counter_collection.csv": "pmc_rdreq.csv",
+              "pmc_dram/run_counter_collection.csv": "pmc_dram.csv", "trace.log": "bench_under_rocprof.log"}
     for s, d in copies.items():
         if os.path.exists(os.path.join(a.src, s)):
             shutil.copy(os.path.join(a.src, s), os.path.join(a.dst, d))
-    fetch = counter_values(os.path.join(a.src, "pmc_fetch/run_counter_collection.csv"), "FETCH_SIZE")
-    write = counter_values(os.path.join(a.src, "pmc_write/run_counter_collection.csv"), "WRITE_SIZE")
+    j = lambda sub: os.path.join(a.src, sub, "run_counter_collection.csv")  # noqa: E731
+    fetch = med(counter_values(j("pmc_fetch"), a.kernel, "FETCH_SIZE"))
+    write = med(counter_values(j("pmc_write"), a.kernel, "WRITE_SIZE"))
+    n32 = med(counter_values(j("pmc_rdreq"), a.kernel, "TCC_EA0_RDREQ_32B_sum"))
+    n64 = med(counter_values(j("pmc_rdreq"), a.kernel, "TCC_EA0_RDREQ_64B_sum"))
+    n128 = med(counter_values(j("pmc_rdreq"), a.kernel, "TCC_EA0_RDREQ_128B_sum"))
+    dram32 = med(counter_values(j("pmc_dram"), a.kernel, "TCC_EA0_RDREQ_DRAM_32B_sum"))
     ver = None
     with open(os.path.join(a.src, "trace.log")) as f:
         for line in f:
             if line.startswith("{"):
-                d = json.loads(line)
-                ver = d.get("engine_version", ver)
-    if ver is None:   # bench logs before engine_version was printed: the in-tree build's
-        import sys
-        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        from svtrek_amd import version
-        ver = version()
-    fk, wk = statistics.median(fetch), statistics.median(write)
+                ver = json.loads(line).get("engine_version", ver)
+    if n128 is not None:
+        rd = 32 * (n32 or 0) + 64 * (n64 or 0) + 128 * n128
+        method_rd = "TCC_EA0_RDREQ_{32B,64B,128B}_sum x {32,64,128} B"
+    else:
+        rd = 2 * fetch * 1024
+        method_rd = "2 x FETCH_SIZE"
     out = {
-        "kernel": KERNEL,
+        "kernel": a.kernel,
         "workload": a.workload,
         "engine_version": ver,
-        "launches": len(fetch),
-        "fetch_size_kb_raw": fk,
-        "write_size_kb_raw": wk,
-        "hbm_bytes_per_launch": int(round(2 * fk * 1024 + wk * 1024)),
-        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_profile.sh); "
-                  "FETCH_SIZE x2 for 16-B-per-lane streaming loads on gfx950 (MI355X_MICROARCH.md, HBM section), "
-                  "WRITE_SIZE as read; median over the profiled launches",
-        "source": f"{a.dst}/pmc_fetch_size.csv, {a.dst}/pmc_write_size.csv",
+        "read_bytes_per_launch": int(round(rd)),
+        "write_bytes_per_launch": int(round((write or 0) * 1024)),
+        "hbm_bytes_per_launch": int(round(rd + (write or 0) * 1024)),
+        "fetch_size_kb_raw": fetch,
+        "write_size_kb_raw": write,
+        "rdreq": {"32B": n32, "64B": n64, "128B": n128},
+        "dram_rdreq_32B_units": dram32,
+        "method": f"rocprofv3 --pmc passes of tools/gpu_profile.sh, one counter group per pass; reads: {method_rd} "
+                  "(2 x FETCH_SIZE agrees: gfx950 tallies a 128-B request at 64 B); writes: WRITE_SIZE; "
+                  "median over the profiled launches",
+        "source": f"{a.dst}/pmc_*.csv",
     }
     with open(os.path.join(os.path.dirname(a.dst.rstrip("/")), "traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
