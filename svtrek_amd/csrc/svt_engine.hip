@@ -35,7 +35,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.0 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.1 (gfx950, event walk)"
 
 namespace {
 
@@ -72,7 +72,8 @@ struct DevPileup {
     const uint2 *bkt;         // {first read with pos >= b << BKT_SHIFT, first read with emax >= b << BKT_SHIFT}
     const uint32_t *cigar;    // padded by CIGAR_PAD zero words
     const uint32_t *chunk;    // [arena words / CHUNK] chunk index (CH_POS | CH_HEAD | CH_DEL | CH_INS)
-    const uint4 *rec2;        // [n_reads] {walk end, candidate-op count, event offset lo, hi}
+    const uint4 *rec2;        // [n_reads] {walk end, candidate-op count, first candidate op (ev[evoff[r]])}
+    const uint64_t *evoff;    // [n_reads] offset of the read's candidate ops in ev
     const uint2 *ev;          // candidate ops of every read in op order: {walk position before the op, CIGAR word}
     int32_t n_targets;
 };
@@ -999,22 +1000,23 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
         }
         // candidate ops processed before the break (refinement.c:124-136 / :190-200 / :299-310)
         {
-            const uint2 *evp = P.ev + ((uint64_t)r2.w << 32 | r2.z);
             uint32_t n = live ? r2.y : 0u;
-            uint2 a = n > 0 ? evp[0] : make_uint2(0, 0), b = n > 1 ? evp[1] : make_uint2(0, 0);
-            for (uint32_t k = 0; ballot(k < n); k += 2) {
-                if (k < n) {
-                    if (a.x > e) n = k;
-                    else if (is_candidate_op<KIND>(a.y & 0xfu, a.y >> 4))
-                        sink.push1(KIND == K_END ? (int32_t)(a.x + (a.y >> 4) + 1u) : (int32_t)a.x);
+            // the first one is inline in rec2 (most reads carry at most one)
+            auto take = [&](uint2 a, uint32_t k) {
+                if (a.x > e) n = k;
+                else if (is_candidate_op<KIND>(a.y & 0xfu, a.y >> 4))
+                    sink.push1(KIND == K_END ? (int32_t)(a.x + (a.y >> 4) + 1u) : (int32_t)a.x);
+            };
+            if (n > 0) take(make_uint2(r2.z, r2.w), 0);
+            if (ballot(n > 1)) {
+                const uint2 *evp = P.ev + (n > 1 ? P.evoff[r] : 0ull);
+                uint2 a = n > 1 ? evp[1] : make_uint2(0, 0), b = n > 2 ? evp[2] : make_uint2(0, 0);
+                for (uint32_t k = 1; ballot(k < n); k += 2) {
+                    if (k < n) take(a, k);
+                    if (k + 1 < n) take(b, k + 1);
+                    a = k + 2 < n ? evp[k + 2] : make_uint2(0, 0);
+                    b = k + 3 < n ? evp[k + 3] : make_uint2(0, 0);
                 }
-                if (k + 1 < n) {
-                    if (b.x > e) n = k + 1;
-                    else if (is_candidate_op<KIND>(b.y & 0xfu, b.y >> 4))
-                        sink.push1(KIND == K_END ? (int32_t)(b.x + (b.y >> 4) + 1u) : (int32_t)b.x);
-                }
-                a = k + 2 < n ? evp[k + 2] : make_uint2(0, 0);
-                b = k + 3 < n ? evp[k + 3] : make_uint2(0, 0);
             }
         }
         // soft-clip candidates at the walk's stop
@@ -1486,7 +1488,6 @@ __global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__
     const int ln = lane_id();
     const uint4 rc = rec[r];
     const uint64_t n = rc.z & NCIG_MASK, src = poff[r], o0 = evoff[r];
-    if (ln == 0) rec2[r].z = (uint32_t)o0, rec2[r].w = (uint32_t)(o0 >> 32);
     if (evoff[r + 1] == o0) return;
     uint32_t carry = rc.x;
     uint64_t k = o0;
@@ -1500,6 +1501,7 @@ __global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__
         if (c) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             ev[k + rank] = make_uint2(after - adv, w);
+            if (k + rank == o0) rec2[r].z = after - adv, rec2[r].w = w;   // the first one, inline
         }
         k += (uint64_t)__popcll(m);
         carry = rdlane(after, WAVE - 1);
@@ -1526,6 +1528,7 @@ struct svt_ctx {
     uint32_t *d_cigar = nullptr;
     uint32_t *d_chunk = nullptr;
     uint4 *d_rec2 = nullptr;
+    uint64_t *d_evoff = nullptr;
     uint2 *d_ev = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
@@ -1562,14 +1565,14 @@ void hfree(T *&p) {
 void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar); hfree(c->d_chunk);
-    hfree(c->d_rec2); hfree(c->d_ev);
+    hfree(c->d_rec2); hfree(c->d_evoff); hfree(c->d_ev);
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
-                       c->d_cigar, c->d_chunk, c->d_rec2, c->d_ev, c->n_targets};
+                       c->d_cigar, c->d_chunk, c->d_rec2, c->d_evoff, c->d_ev, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
                     c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
     a.loci = d_loci;
@@ -1761,13 +1764,13 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
         // pass 1 (pack_kernel): padded arena, chunk index, walk ends, candidate-op counts;
         // host: exclusive scan of the counts; pass 2 (event_kernel): the candidate-op lists
         uint32_t *d_raw = nullptr, *d_nev = nullptr;
-        uint64_t *d_raw_off = nullptr, *d_evoff = nullptr;
+        uint64_t *d_raw_off = nullptr;
         std::vector<uint32_t> nev((size_t)nr);
         std::vector<uint64_t> evoff((size_t)nr + 1, 0);
         hipError_t e = hipMalloc(&d_raw, std::max<uint64_t>(nops, 1) * 4);
         if (e == hipSuccess) e = hipMalloc(&d_raw_off, ((size_t)nr + 1) * 8);
         if (e == hipSuccess) e = hipMalloc(&d_nev, (size_t)nr * 4);
-        if (e == hipSuccess) e = hipMalloc(&d_evoff, ((size_t)nr + 1) * 8);
+        if (e == hipSuccess) e = hipMalloc(&c->d_evoff, ((size_t)nr + 1) * 8);
         if (e == hipSuccess && nops) e = hipMemcpy(d_raw, p->cigar, nops * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
         if (e == hipSuccess) {
@@ -1781,20 +1784,21 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
         hfree(d_nev);
         if (e == hipSuccess) {
             for (int64_t r = 0; r < nr; r++) evoff[(size_t)r + 1] = evoff[(size_t)r] + nev[(size_t)r];
-            e = hipMemcpy(d_evoff, evoff.data(), ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
+            e = hipMemcpy(c->d_evoff, evoff.data(), ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
+            c->dev_bytes += ((size_t)nr + 1) * 8;
         }
         if (e == hipSuccess) e = hipMalloc(&c->d_ev, std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2));
         if (e == hipSuccess) {
             c->dev_bytes += std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2);
             hipLaunchKernelGGL(event_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
-                               c->d_off64, c->d_rec, c->d_rec2, d_evoff, c->d_ev, (int64_t)nr);
+                               c->d_off64, c->d_rec, c->d_rec2, c->d_evoff, c->d_ev, (int64_t)nr);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipDeviceSynchronize();
-        hfree(d_evoff);
         if (e != hipSuccess) return fail(c, SVT_EDEVICE, "pileup pack: %s", hipGetErrorString(e));
-    } else if ((s = upload<uint2>(c, c->d_ev, nullptr, 0, 1))) {
-        return s;
+    } else {
+        if ((s = upload<uint2>(c, c->d_ev, nullptr, 0, 1))) return s;
+        if ((s = upload<uint64_t>(c, c->d_evoff, nullptr, 0, 1))) return s;
     }
     c->n_targets = nt;
     c->n_reads = nr;
