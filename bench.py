@@ -92,6 +92,8 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--scale", type=float, default=1.0,
+                    help="diagnostic: scale the workload's locus count (and so its genome) by this factor")
     ap.add_argument("--replicate", type=int, default=1,
                     help="diagnostic: launch the workload's loci R times per step (tail-effect study)")
     args = ap.parse_args()
@@ -114,6 +116,9 @@ def main() -> int:
 
     # ---- synthetic workload (BASELINE config), one shard per rank (weak scaling)
     cfg = sim.WORKLOADS[args.workload]
+    if args.scale != 1.0:
+        from dataclasses import replace
+        cfg = replace(cfg, n_loci=max(1, int(cfg.n_loci * args.scale)))
     if world > 1:
         from dataclasses import replace
         cfg = replace(cfg, seed=cfg.seed + 1000 * rank)
@@ -221,7 +226,8 @@ def main() -> int:
             "config": {"workload": args.workload, "loci_per_gpu": n, "reads_per_gpu": res.pileup.n_reads,
                        "cigar_ops_per_gpu": res.pileup.n_ops, "coverage": cfg.coverage,
                        "read_len_mean": cfg.read_len_mean, "parallelism": f"loci-shard x{world}",
-                       "gather": bool(world > 1 and not args.no_gather)},
+                       "gather": bool(world > 1 and not args.no_gather),
+                       **({"loci_scale": args.scale} if args.scale != 1.0 else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_gbs": round(traffic / (kern_mean_ms * 1e-3) / 1e9, 2) if traffic else None,

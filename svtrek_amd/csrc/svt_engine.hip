@@ -35,7 +35,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.1 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.2 (gfx950, event walk)"
 
 namespace {
 
@@ -1078,6 +1078,44 @@ __device__ __forceinline__ void wave_bitonic_sort(int32_t *buf, int N) {
     }
 }
 
+// Bitonic sort of buf[0..n), n <= 64*E, in registers: element i = k*64 + lane lives in x[k];
+// exchanges at distance >= 64 stay inside a lane, shorter ones are lane-xor shuffles.
+// Padding is INT32_MAX; one load and one store per element.
+template <int E>
+__device__ __forceinline__ void reg_bitonic_sort(int32_t *buf, int32_t n) {
+    const int ln = lane_id();
+    int32_t x[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) x[k] = k * WAVE + ln < n ? buf[k * WAVE + ln] : INT32_MAX;
+#pragma unroll
+    for (int kk = 2; kk <= E * WAVE; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= WAVE) {
+                const int kj = j / WAVE;
+#pragma unroll
+                for (int k = 0; k < E; k++) {
+                    if (k & kj) continue;
+                    const bool asc = ((k * WAVE + ln) & kk) == 0;
+                    const int32_t a = x[k], b = x[k | kj];
+                    x[k] = asc ? min(a, b) : max(a, b);
+                    x[k | kj] = asc ? max(a, b) : min(a, b);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < E; k++) {
+                    const int i = k * WAVE + ln;
+                    const int32_t y = __shfl_xor(x[k], j, WAVE);
+                    x[k] = (((i & j) == 0) == ((i & kk) == 0)) ? min(x[k], y) : max(x[k], y);
+                }
+            }
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < E; k++) buf[k * WAVE + ln] = x[k];
+}
+
 __device__ __forceinline__ int32_t ref_abs(int32_t a) { return a < 0 ? -a : a; }   // refinement.h:41
 
 __device__ __forceinline__ int32_t first_greater(const int32_t *buf, int32_t l, int32_t h, int64_t key) {
@@ -1224,21 +1262,10 @@ template <int VOTE>
 __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
                                                  int32_t &support) {
     const int ln = lane_id();
-    if (n <= WAVE) {
-        // one value per lane: bitonic network in registers (lane-xor exchanges), then one
-        // store of the sorted values
-        int32_t x = ln < n ? buf[ln] : INT32_MAX;
-#pragma unroll
-        for (int kk = 2; kk <= WAVE; kk <<= 1) {
-#pragma unroll
-            for (int j = kk >> 1; j > 0; j >>= 1) {
-                const int32_t y = __shfl_xor(x, j, WAVE);
-                x = (((ln & j) == 0) == ((ln & kk) == 0)) ? min(x, y) : max(x, y);
-            }
-        }
-        wave_sync();
-        buf[ln] = x;
-    } else {
+    if (n <= WAVE) reg_bitonic_sort<1>(buf, n);
+    else if (n <= 2 * WAVE) reg_bitonic_sort<2>(buf, n);
+    else if (n <= 4 * WAVE) reg_bitonic_sort<4>(buf, n);
+    else {
         int N = 1;
         while (N < n) N <<= 1;
         for (int i = n + ln; i < N; i += WAVE) buf[i] = INT32_MAX;

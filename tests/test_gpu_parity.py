@@ -266,3 +266,26 @@ def test_wrapping_walks_take_exact_path(engine_factory):
         got = eng.refine(loci)
         want = O.refine_batch(pl, loci)
         _assert_same(got, want, loci)
+
+
+@pytest.mark.parametrize("ncand", [63, 64, 65, 100, 128, 129, 200, 256])
+def test_register_sort_sizes(engine_factory, ncand):
+    """Candidate counts around the register-sort tiers (64 / 128 / 256 per window) and the
+    LDS capacity: same votes as the oracle."""
+    rng = np.random.default_rng(ncand)
+    base = 500000
+    rows, vals = [], []
+    for k in range(30):
+        c = base + k * 80000
+        centers = c + rng.integers(-300, 300, size=4)
+        vals.extend(int(rng.choice(centers)) + int(rng.integers(-6, 7)) for _ in range(ncand))
+        rows.append((2, 1, c + int(rng.integers(-20, 20)), c + 30000))
+    pl = cluster_pileup(vals)
+    eng = engine_factory(Params(consensus_min_count=2))
+    eng.load_pileup(pl)
+    loci = make_loci(rows)
+    w = eng.count_work(loci)
+    assert w["spilled_windows"] == 0
+    got = eng.refine(loci)
+    want = O.refine_batch(pl, loci, eng.params)
+    _assert_same(got, want, loci)
