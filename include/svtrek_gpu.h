@@ -158,6 +158,51 @@ uint64_t   svt_sw_subwindows(const svt_sw_query *q, int32_t window_size);
 svt_status svt_sliding_window_ins(svt_ctx *ctx, const svt_sw_query *q, size_t n, int32_t window_size,
                                   int32_t slide_size, int32_t *best, svt_sw_window *sub);
 
+/* ---- optional mode: allele consensus of refined INS calls (POA) ----------------------
+ * The north star's "abPOA banded partial-order consensus" step.  The reference declares
+ * abPOA as a submodule (.gitmodules:4-6) but never includes or calls it (Makefile:16
+ * links -lhts -lz -pthread only), so this mode has NO reference behaviour (parity
+ * unpinned; its checker is oracle/poa_oracle.c) and never changes refined breakpoints.
+ *
+ * Sequences: the inserted bases of every I op with len >= 50 in the loaded pileup, in
+ * (read, op) order of that pileup, as nt4 codes (0 A, 1 C, 2 G, 3 T, 4 other); sequence k
+ * is bases[off[k] .. off[k+1]) and its length is the op's len.  For an INS call refined to
+ * R, the supporting sequences are those I >= 50 ops of refine_ins's window reads
+ * (refinement.c:290-316) processed by its walk, |position - R| <= support_radius and
+ * len <= max_len, in read then op order; the first max_support are kept, the first
+ * max_seqs that fit are fused (banded POA, w = band_b + band_f_permille * len / 1000), and
+ * the heaviest bundle of the graph is the consensus. */
+typedef struct svt_insseq_view {
+    uint64_t        n_ins;   /* must equal svt_pileup_ins_count()                         */
+    const uint64_t *off;     /* [n_ins + 1]                                               */
+    const uint8_t  *bases;   /* [off[n_ins]] nt4 codes                                     */
+} svt_insseq_view;
+
+typedef struct svt_poa_params {
+    int32_t match, mismatch, gap_open, gap_ext;  /* 2, 4, 4, 2 (a gap of L costs open + L*ext) */
+    int32_t band_b, band_f_permille;             /* 10, 10; band_b + band_f * max_len / 1000 <= 63 */
+    int32_t max_seqs, max_len, max_nodes;        /* 32 (<= 32), 4000 (<= 4096), 32768 (<= 65000) */
+    int32_t support_radius, max_support;         /* 20, 64                                     */
+} svt_poa_params;
+
+typedef struct svt_poa_result {
+    int32_t len;        /* consensus length (bases[0 .. min(len, cap)) written); -1: not a refined INS */
+    int32_t n_support;  /* supporting sequences found                                     */
+    int32_t n_used;     /* sequences fused into the graph                                 */
+    int32_t status;     /* 0                                                              */
+} svt_poa_result;
+
+void       svt_poa_default_params(svt_poa_params *p);
+/* I >= 50 ops in the loaded pileup (the length svt_load_insseq expects). */
+uint64_t   svt_pileup_ins_count(const svt_ctx *ctx);
+/* Copy the insertion sequences to the device (after svt_load_pileup).  Synchronous. */
+svt_status svt_load_insseq(svt_ctx *ctx, const svt_insseq_view *seqs);
+/* Consensus for n loci with their refined results (svt_refine_batch output): INS loci with a
+ * refined start get a consensus in bases[i*cap ..], others len = -1.  Synchronous. */
+svt_status svt_poa_consensus(svt_ctx *ctx, const svt_poa_params *p, const svt_locus *loci,
+                             const svt_result *refined, size_t n, int32_t cap, uint8_t *bases,
+                             svt_poa_result *res);
+
 /* Bytes of device memory the loaded pileup occupies. */
 uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
 

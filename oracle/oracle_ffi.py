@@ -138,3 +138,60 @@ def sliding_window_ins(pl, chrom: int, start: int, end: int, window_size: int, s
                                         slide_size, min_count, cand.ctypes.data, sup.ctypes.data)
     del keep
     return best, cand, sup
+
+
+# ---------------------------------------------------------------- allele consensus (POA)
+POA_FIELDS = ("match", "mismatch", "gap_open", "gap_ext", "band_b", "band_f_permille", "max_seqs", "max_len",
+              "max_nodes", "support_radius", "max_support")
+POA_DEFAULTS = dict(match=2, mismatch=4, gap_open=4, gap_ext=2, band_b=10, band_f_permille=10, max_seqs=32,
+                    max_len=4000, max_nodes=32768, support_radius=20, max_support=64)
+
+
+class OrcPoaParams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in POA_FIELDS]
+
+
+def poa_params(**kw) -> OrcPoaParams:
+    d = dict(POA_DEFAULTS)
+    d.update(kw)
+    return OrcPoaParams(*(d[n] for n in POA_FIELDS))
+
+
+def _poa_lib():
+    L = lib()
+    if not getattr(L, "_poa_bound", False):
+        P = C.c_void_p
+        L.orc_poa_consensus.argtypes = [P, P, C.c_int, P, P, C.c_int, P]
+        L.orc_poa_consensus.restype = C.c_int
+        L.orc_poa_support.argtypes = [P, P, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, P, P, C.c_int]
+        L.orc_poa_support.restype = C.c_int
+        L._poa_bound = True
+    return L
+
+
+def poa_consensus(seqs, cap: int = 1 << 16, **kw) -> tuple[np.ndarray, int]:
+    """Consensus (nt4 uint8 array) of the sequences, in order, and how many were fused."""
+    L = _poa_lib()
+    off = np.zeros(len(seqs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(s) for s in seqs])
+    bases = np.concatenate([np.asarray(s, dtype=np.uint8) for s in seqs]) if seqs else np.zeros(1, np.uint8)
+    out = np.zeros(cap, dtype=np.uint8)
+    used = C.c_int32(0)
+    pp = poa_params(**kw)
+    n = L.orc_poa_consensus(bases.ctypes.data, off.ctypes.data, len(seqs), C.byref(pp), out.ctypes.data, cap,
+                            C.byref(used))
+    if n < 0:
+        raise MemoryError("orc_poa_consensus")
+    return out[:min(n, cap)].copy(), int(used.value)
+
+
+def poa_support(pl, ins_base: np.ndarray, chrom: int, s: int, e: int, refined: int, cap: int = 64, **kw) -> np.ndarray:
+    L = _poa_lib()
+    v, keep = pileup(pl)
+    ib = np.ascontiguousarray(ins_base, dtype=np.uint64)
+    idx = np.zeros(cap, dtype=np.int64)
+    pp = poa_params(**kw)
+    n = L.orc_poa_support(C.byref(v), ib.ctypes.data, chrom, s & 0xFFFFFFFF, e & 0xFFFFFFFF, refined & 0xFFFFFFFF,
+                          C.byref(pp), idx.ctypes.data, cap)
+    del keep
+    return idx[:min(n, cap)].copy()

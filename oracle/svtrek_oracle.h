@@ -68,6 +68,23 @@ int  orc_refine_batch(const orc_pileup *p, const orc_params *prm, const orc_locu
 int orc_sliding_window_ins(const orc_pileup *p, int chrom, uint32_t start, uint32_t end, int window_size,
                            int slide_size, int min_count, int32_t *sub_cand, int32_t *sub_support);
 
+/* Allele consensus (POA; no reference behaviour -- parity unpinned, see poa_oracle.c). */
+typedef struct orc_poa_params {
+    int32_t match, mismatch, gap_open, gap_ext;   /* 2, 4, 4, 2 */
+    int32_t band_b, band_f_permille;              /* band w = b + f*len: 10, 10 (= 0.01) */
+    int32_t max_seqs, max_len, max_nodes;         /* 32, 4000, 32768 */
+    int32_t support_radius, max_support;          /* 20, 64 */
+} orc_poa_params;
+
+/* Consensus of nseq nt4 sequences (bases[off[i] .. off[i+1])), in order; returns its
+ * length (written up to cap), -1 on allocation failure; *nused = sequences fused. */
+int orc_poa_consensus(const uint8_t *bases, const uint64_t *off, int nseq, const orc_poa_params *pp,
+                      uint8_t *out, int cap, int32_t *nused);
+/* Supporting I ops (global indices into the insertion-sequence arrays) of an INS call
+ * refined to `refined` over window [s, e]; returns the count (first cap written). */
+int orc_poa_support(const orc_pileup *p, const uint64_t *ins_base, int chrom, uint32_t s, uint32_t e,
+                    uint32_t refined, const orc_poa_params *pp, int64_t *idx, int cap);
+
 /* A1: parse one VCF data line (modified in place, as strtok_r does).  Returns
  * 1 = record reaches the type switch (*l filled), 0 = skipped silently,
  * 2 = skipped with a stderr message (text copied into err). */

@@ -54,6 +54,18 @@ class SvtPileupView(C.Structure):
     ]
 
 
+class SvtPoaParams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("match", "mismatch", "gap_open", "gap_ext", "band_b", "band_f_permille",
+                                          "max_seqs", "max_len", "max_nodes", "support_radius", "max_support")]
+
+
+class SvtInsseqView(C.Structure):
+    _fields_ = [("n_ins", C.c_uint64), ("off", C.c_void_p), ("bases", C.c_void_p)]
+
+
+POA_RESULT_DTYPE = np.dtype([("len", "<i4"), ("n_support", "<i4"), ("n_used", "<i4"), ("status", "<i4")])
+
+
 class SvtWork(C.Structure):
     _fields_ = [
         ("windows", C.c_uint64),
@@ -69,6 +81,7 @@ ENGINE_SYMBOLS = (
     "svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
     "svt_count_work", "svt_pileup_device_bytes", "svt_last_error", "svt_close", "svt_version",
     "svt_sw_subwindows", "svt_sliding_window_ins",
+    "svt_poa_default_params", "svt_pileup_ins_count", "svt_load_insseq", "svt_poa_consensus",
 )
 
 _engine = None
@@ -105,8 +118,14 @@ def load_engine() -> C.CDLL:
     lib.svt_sw_subwindows.argtypes = [P, C.c_int32]
     lib.svt_sw_subwindows.restype = C.c_uint64
     lib.svt_sliding_window_ins.argtypes = [P, P, C.c_size_t, C.c_int32, C.c_int32, P, P]
+    lib.svt_poa_default_params.argtypes = [C.POINTER(SvtPoaParams)]
+    lib.svt_poa_default_params.restype = None
+    lib.svt_pileup_ins_count.argtypes = [P]
+    lib.svt_pileup_ins_count.restype = C.c_uint64
+    lib.svt_load_insseq.argtypes = [P, C.POINTER(SvtInsseqView)]
+    lib.svt_poa_consensus.argtypes = [P, C.POINTER(SvtPoaParams), P, P, C.c_size_t, C.c_int32, P, P]
     for name in ("svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
-                 "svt_count_work", "svt_sliding_window_ins"):
+                 "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):
         getattr(lib, name).restype = C.c_int32
     _engine = lib
     return lib
@@ -140,6 +159,11 @@ def load_sim() -> C.CDLL:
         getattr(lib, name).restype = P
     lib.sim_write_bam.argtypes = [P, C.c_char_p, C.c_int, C.c_int]
     lib.sim_write_bam.restype = C.c_int
+    lib.sim_insseq.argtypes = [P, C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(P),
+                               C.POINTER(P)]
+    lib.sim_insseq.restype = C.c_int
+    lib.sim_free_buf.argtypes = [P]
+    lib.sim_free_buf.restype = None
     _sim = lib
     return lib
 

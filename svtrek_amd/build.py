@@ -39,7 +39,7 @@ def _stale(out: str, deps: list[str]) -> bool:
 
 def build_engine(force: bool = False) -> str:
     out = os.path.join(PKG, "libsvtrek_hip.so")
-    deps = [os.path.join(CSRC, "svt_engine.hip"), os.path.join(INC, "svtrek_gpu.h")]
+    deps = [os.path.join(CSRC, "svt_engine.hip"), os.path.join(INC, "svtrek_gpu.h"), os.path.join(CSRC, "svt_poa.inc")]
     if force or _stale(out, deps):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
               "-Wall", "-I", INC, "-o", out, deps[0]])
@@ -80,7 +80,7 @@ def build_sim(force: bool = False) -> str:
 def build_oracle(force: bool = False) -> str:
     """Test infrastructure: the CPU parity oracle (oracle/Makefile)."""
     out = os.path.join(ROOT, "oracle", "liboracle.so")
-    src = [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "svtrek_oracle.h")]
+    src = [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "poa_oracle.c", "svtrek_oracle.h", "Makefile")]
     if force or _stale(out, src):
         _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + (["-B"] if force else []))
     return out

@@ -380,6 +380,82 @@ int32_t sim_n_loci(const sim_pileup *p) { return p->n_loci; }
 const int32_t *sim_loci(const sim_pileup *p) { return p->loci; }
 const int32_t *sim_truth(const sim_pileup *p) { return p->truth; }
 
+/* ---------------------------------------------------------------- insertion sequences */
+typedef struct { int32_t bp1, len, k; } ins_key;
+
+static int cmp_ins(const void *a, const void *b) {
+    const ins_key *x = (const ins_key *)a, *y = (const ins_key *)b;
+    return x->bp1 < y->bp1 ? -1 : x->bp1 > y->bp1 ? 1 : (x->k < y->k ? -1 : x->k > y->k);
+}
+
+void sim_free_buf(void *x) { free(x); }
+
+int sim_insseq(const sim_pileup *p, uint64_t seed, int32_t bp_jitter, int32_t err_permille, uint64_t *n_ins,
+               uint64_t **off_out, uint8_t **bases_out) {
+    *n_ins = 0; *off_out = NULL; *bases_out = NULL;
+    /* INS loci per contig, sorted by true bp1 */
+    int32_t nt = p->n_targets;
+    ins_key *keys = (ins_key *)malloc(sizeof(ins_key) * (size_t)(p->n_loci > 0 ? p->n_loci : 1));
+    int64_t *koff = (int64_t *)calloc((size_t)nt + 1, sizeof(int64_t));
+    if (!keys || !koff) { free(keys); free(koff); return -1; }
+    int64_t nk = 0;
+    for (int32_t t = 0; t < nt; t++) {
+        koff[t] = nk;
+        for (int32_t k = 0; k < p->n_loci; k++)
+            if (p->loci[4 * k] == 1 && p->loci[4 * k + 1] == t + 1)
+                keys[nk++] = (ins_key){p->truth[2 * k], p->truth[2 * k + 1] - p->truth[2 * k], k};
+        qsort(keys + koff[t], (size_t)(nk - koff[t]), sizeof(ins_key), cmp_ins);
+    }
+    koff[nt] = nk;
+    /* pass 1: sizes */
+    uint64_t n = 0, nb = 0;
+    for (int64_t r = 0; r < p->n_reads; r++)
+        for (uint64_t i = p->cig_off[r]; i < p->cig_off[r + 1]; i++)
+            if ((p->cigar[i] & 0xfu) == OP_I && (p->cigar[i] >> 4) >= 50) { n++; nb += p->cigar[i] >> 4; }
+    uint64_t *off = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n + 1));
+    uint8_t *bases = (uint8_t *)malloc((size_t)(nb > 0 ? nb : 1));
+    if (!off || !bases) { free(off); free(bases); free(keys); free(koff); return -1; }
+    /* pass 2 */
+    uint64_t q = 0, o = 0;
+    rng_t rng;
+    rng_seed(&rng, seed ^ 0x9e3779b97f4a7c15ull);
+    for (int32_t t = 0; t < nt; t++) {
+        for (int64_t r = p->tid_off[t]; r < p->tid_off[t + 1]; r++) {
+            uint32_t rp = (uint32_t)p->pos[r];
+            for (uint64_t i = p->cig_off[r]; i < p->cig_off[r + 1]; i++) {
+                const uint32_t op = p->cigar[i] & 0xfu, len = p->cigar[i] >> 4;
+                if (op == OP_I && len >= 50) {
+                    off[q++] = o;
+                    /* the INS locus whose allele this op carries, if any */
+                    int64_t lo = koff[t], hi = koff[t + 1];
+                    while (lo < hi) { int64_t m = (lo + hi) / 2; if ((int64_t)keys[m].bp1 < (int64_t)rp - bp_jitter - 1) lo = m + 1; else hi = m; }
+                    int32_t k = -1;
+                    for (int64_t m = lo; m < koff[t + 1] && (int64_t)keys[m].bp1 <= (int64_t)rp + bp_jitter + 1; m++)
+                        if (keys[m].len == (int32_t)len) { k = keys[m].k; break; }
+                    if (k >= 0) {
+                        rng_t al;   /* the locus's allele: a per-locus stream */
+                        rng_seed(&al, seed * 1000003ull + (uint64_t)k);
+                        for (uint32_t b = 0; b < len; b++) {
+                            uint8_t base = (uint8_t)(rng_u64(&al) & 3);
+                            if ((int32_t)(rng_u64(&rng) % 1000) < err_permille)
+                                base = (uint8_t)((base + 1 + rng_u64(&rng) % 3) & 3);
+                            bases[o + b] = base;
+                        }
+                    } else {
+                        for (uint32_t b = 0; b < len; b++) bases[o + b] = (uint8_t)(rng_u64(&rng) & 3);
+                    }
+                    o += len;
+                }
+                if (op != OP_I && op != OP_S) rp += len;
+            }
+        }
+    }
+    off[n] = o;
+    free(keys); free(koff);
+    *n_ins = n; *off_out = off; *bases_out = bases;
+    return 0;
+}
+
 /* ---------------------------------------------------------------- BAM writer */
 typedef struct {
     FILE *f;

@@ -60,6 +60,16 @@ int32_t         sim_n_loci(const sim_pileup *p);
 const int32_t  *sim_loci(const sim_pileup *p);        /* [n_loci*4]                        */
 const int32_t  *sim_truth(const sim_pileup *p);       /* [n_loci*2] true bp1, bp2          */
 
+/* Insertion sequences for the allele-consensus mode: for every I op with len >= 50, in
+ * (read, op) order, `len` nt4 bases (0 A, 1 C, 2 G, 3 T).  An I op carrying an INS locus's
+ * allele (an INS locus of the read's contig whose true bp1 is within bp_jitter + 1 of the
+ * op's walk position and whose length equals the op's) gets that locus's allele (random,
+ * seeded per locus) with per-base substitutions at err_permille / 1000; any other I op gets
+ * random bases.  *off ([n+1]) and *bases are malloc'ed (free with sim_free_buf).  0 / -1. */
+int  sim_insseq(const sim_pileup *p, uint64_t seed, int32_t bp_jitter, int32_t err_permille, uint64_t *n_ins,
+                uint64_t **off, uint8_t **bases);
+void sim_free_buf(void *x);
+
 /* Write the pileup as a BGZF-compressed, coordinate-sorted BAM.  with_seq != 0 stores
  * random SEQ/QUAL of the CIGAR's query length (realistic ingest cost).  0 on success. */
 int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level);

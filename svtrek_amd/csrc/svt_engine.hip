@@ -1475,7 +1475,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
     const uint64_t npad = n ? (n + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1) : (uint64_t)ALIGN_OPS;
     const uint32_t rpos = rec[r].x;
     uint64_t walk = 0;
-    uint32_t carry = rpos, nev = 0;
+    uint32_t carry = rpos, nev = 0, nins = 0;
     for (uint64_t i0 = 0; i0 < npad; i0 += WAVE) {
         const uint64_t i = i0 + (uint64_t)ln;
         const uint32_t w = i < n ? raw[o0 + i] : 0u;
@@ -1493,13 +1493,15 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
         }
         carry = rdlane(after, WAVE - 1);
         nev += (uint32_t)__popcll(dm | im);
+        nins += (uint32_t)__popcll(im);
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) walk += __shfl_xor(walk, d, WAVE);
     if (ln == 0) {
         if ((uint64_t)rpos + walk >= INDEX_LIMIT) rec[r].z |= SLOW_BIT;
         rec2[r] = make_uint4(rpos + (uint32_t)walk, nev, 0u, 0u);
-        nev_out[r] = nev;
+        nev_out[r] = nev;         // candidate ops (D > 50 or I >= 50)
+        nev_out[nr + r] = nins;   // I >= 50 ops (the allele-consensus sequences, svt_load_insseq)
     }
 }
 
@@ -1535,6 +1537,8 @@ __global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__
     }
 }
 
+#include "svt_poa.inc"
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1556,6 +1560,15 @@ struct svt_ctx {
     uint32_t *d_chunk = nullptr;
     uint4 *d_rec2 = nullptr;
     uint64_t *d_evoff = nullptr;
+    uint64_t *d_insbase = nullptr;    // per read: its first I >= 50 op's index in the insertion sequences
+    uint64_t n_ins = 0;               // I >= 50 ops in the pileup
+    // allele-consensus mode (svt_load_insseq / svt_poa_consensus)
+    uint64_t *d_ins_off = nullptr;
+    uint8_t *d_ins_bases = nullptr;
+    bool insseq_loaded = false;
+    uint8_t *d_poa_slots = nullptr;
+    uint64_t poa_slot_bytes = 0;
+    uint32_t poa_nslots = 0;
     uint2 *d_ev = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
@@ -1592,7 +1605,9 @@ void hfree(T *&p) {
 void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar); hfree(c->d_chunk);
-    hfree(c->d_rec2); hfree(c->d_evoff); hfree(c->d_ev);
+    hfree(c->d_rec2); hfree(c->d_evoff); hfree(c->d_ev); hfree(c->d_insbase); hfree(c->d_ins_off);
+    hfree(c->d_ins_bases);
+    c->insseq_loaded = false; c->n_ins = 0;
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
@@ -1661,6 +1676,66 @@ svt_status upload(svt_ctx *c, T *&dst, const T *src, size_t n, size_t pad_elems 
     if (pad_elems) HIP_TRY(c, hipMemset(dst + n, 0, pad_elems * sizeof(T)));
     c->dev_bytes += bytes;
     return SVT_OK;
+}
+
+// POA scratch: one slot per persistent wave, min(batch, POA_SLOTS) slots, kept across calls.
+constexpr uint64_t POA_SLOTS = 256;
+
+svt_status poa_scratch(svt_ctx *c, const svt_poa_params *p, size_t n) {
+    const uint64_t sb = poa_slot_bytes(p->max_nodes, p->max_len, p->max_support);
+    const uint64_t want = std::min<uint64_t>(n, POA_SLOTS);
+    if (c->d_poa_slots && c->poa_slot_bytes == sb && c->poa_nslots >= want) return SVT_OK;
+    hfree(c->d_poa_slots);
+    c->poa_nslots = 0;
+    if (hipMalloc(&c->d_poa_slots, want * sb) != hipSuccess)
+        return fail(c, SVT_ENOMEM, "%s", "poa scratch (lower max_nodes / max_len)");
+    c->poa_slot_bytes = sb;
+    c->poa_nslots = (uint32_t)want;
+    return SVT_OK;
+}
+
+svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, const svt_result *refined, size_t n,
+                   int32_t cap, uint8_t *bases, svt_poa_result *res) {
+    svt_locus *d_loci = nullptr;
+    svt_result *d_ref = nullptr;
+    uint8_t *d_out = nullptr;
+    int4 *d_res = nullptr;
+    svt_status s = SVT_OK;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && s == SVT_OK) s = fail(c, SVT_EDEVICE, what, hipGetErrorString(e));
+        return s == SVT_OK;
+    };
+    if (chk(hipMalloc(&d_loci, n * sizeof(svt_locus)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_ref, n * sizeof(svt_result)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_out, std::max<size_t>(1, n * (size_t)cap)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_res, n * sizeof(int4)), "hipMalloc: %s") &&
+        chk(hipMemcpy(d_loci, loci, n * sizeof(svt_locus), hipMemcpyHostToDevice), "H2D: %s") &&
+        chk(hipMemcpy(d_ref, refined, n * sizeof(svt_result), hipMemcpyHostToDevice), "H2D: %s")) {
+        const KArgs k = make_args(c, nullptr, nullptr, 0, false);
+        PoaArgs a;
+        a.pile = k.pile;
+        a.prm = k.prm;
+        a.pp = PoaParams{p->match, p->mismatch, p->gap_open, p->gap_ext, p->band_b, p->band_f_permille,
+                         p->max_seqs, p->max_len, p->max_nodes, p->support_radius, p->max_support};
+        a.loci = d_loci;
+        a.refined = d_ref;
+        a.n = (uint32_t)n;
+        a.ins_base = c->d_insbase;
+        a.ins_off = c->d_ins_off;
+        a.ins_bases = c->d_ins_bases;
+        a.slots = c->d_poa_slots;
+        a.slot_bytes = c->poa_slot_bytes;
+        a.cap = cap;
+        a.out = d_out;
+        a.res = d_res;
+        const unsigned grid = (unsigned)std::min<uint64_t>(c->poa_nslots, n);
+        hipLaunchKernelGGL(poa_kernel, dim3(grid), dim3(64), 0, nullptr, a);
+        if (chk(hipGetLastError(), "poa_kernel: %s") && chk(hipDeviceSynchronize(), "poa_kernel: %s") &&
+            chk(hipMemcpy(res, d_res, n * sizeof(int4), hipMemcpyDeviceToHost), "D2H: %s") && cap > 0)
+            chk(hipMemcpy(bases, d_out, n * (size_t)cap, hipMemcpyDeviceToHost), "D2H: %s");
+    }
+    hfree(d_loci); hfree(d_ref); hfree(d_out); hfree(d_res);
+    return s;
 }
 
 }  // namespace
@@ -1792,11 +1867,11 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
         // host: exclusive scan of the counts; pass 2 (event_kernel): the candidate-op lists
         uint32_t *d_raw = nullptr, *d_nev = nullptr;
         uint64_t *d_raw_off = nullptr;
-        std::vector<uint32_t> nev((size_t)nr);
+        std::vector<uint32_t> nev((size_t)nr * 2);
         std::vector<uint64_t> evoff((size_t)nr + 1, 0);
         hipError_t e = hipMalloc(&d_raw, std::max<uint64_t>(nops, 1) * 4);
         if (e == hipSuccess) e = hipMalloc(&d_raw_off, ((size_t)nr + 1) * 8);
-        if (e == hipSuccess) e = hipMalloc(&d_nev, (size_t)nr * 4);
+        if (e == hipSuccess) e = hipMalloc(&d_nev, (size_t)nr * 8);
         if (e == hipSuccess) e = hipMalloc(&c->d_evoff, ((size_t)nr + 1) * 8);
         if (e == hipSuccess && nops) e = hipMemcpy(d_raw, p->cigar, nops * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
@@ -1805,12 +1880,23 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
                                c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, c->d_rec2, d_nev, (int64_t)nr);
             e = hipGetLastError();
         }
-        if (e == hipSuccess) e = hipMemcpy(nev.data(), d_nev, (size_t)nr * 4, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(nev.data(), d_nev, (size_t)nr * 8, hipMemcpyDeviceToHost);
         hfree(d_raw);
         hfree(d_raw_off);
         hfree(d_nev);
         if (e == hipSuccess) {
             for (int64_t r = 0; r < nr; r++) evoff[(size_t)r + 1] = evoff[(size_t)r] + nev[(size_t)r];
+            // each read's first I >= 50 op in the pileup-wide (read, op) order of the
+            // allele-consensus sequences (svt_load_insseq)
+            std::vector<uint64_t> ib((size_t)nr);
+            uint64_t acc = 0;
+            for (int64_t r = 0; r < nr; r++) { ib[(size_t)r] = acc; acc += nev[(size_t)nr + (size_t)r]; }
+            c->n_ins = acc;
+            e = hipMalloc(&c->d_insbase, (size_t)nr * 8);
+            if (e == hipSuccess) e = hipMemcpy(c->d_insbase, ib.data(), (size_t)nr * 8, hipMemcpyHostToDevice);
+            if (e == hipSuccess) c->dev_bytes += (size_t)nr * 8;
+        }
+        if (e == hipSuccess) {
             e = hipMemcpy(c->d_evoff, evoff.data(), ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
             c->dev_bytes += ((size_t)nr + 1) * 8;
         }
@@ -1964,13 +2050,63 @@ svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, i
     return s;
 }
 
+// ---- allele-consensus mode (POA; no reference behaviour, see svt_poa.inc)
+void svt_poa_default_params(svt_poa_params *p) {
+    if (p) *p = svt_poa_params{2, 4, 4, 2, 10, 10, 32, 4000, 32768, 20, 64};
+}
+
+uint64_t svt_pileup_ins_count(const svt_ctx *c) { return c ? c->n_ins : 0; }
+
+svt_status svt_load_insseq(svt_ctx *c, const svt_insseq_view *v) {
+    if (!c || !v) return SVT_EINVAL;
+    if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
+    if (v->n_ins != c->n_ins) return fail(c, SVT_EINVAL, "insseq: %s", "n_ins differs from the pileup's I >= 50 op count");
+    if (v->n_ins >= (1ull << 31)) return fail(c, SVT_EINVAL, "insseq: %s", ">= 2^31 sequences");
+    if (v->n_ins && (!v->off || !v->bases)) return fail(c, SVT_EINVAL, "insseq: %s", "missing arrays");
+    if (v->n_ins && v->off[0] != 0) return fail(c, SVT_EINVAL, "insseq: %s", "off[0] != 0");
+    for (uint64_t k = 0; k < v->n_ins; k++)
+        if (v->off[k + 1] < v->off[k]) return fail(c, SVT_EINVAL, "insseq: %s", "off not monotone");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hfree(c->d_ins_off);
+    hfree(c->d_ins_bases);
+    c->insseq_loaded = false;
+    const uint64_t nb = v->n_ins ? v->off[v->n_ins] : 0;
+    svt_status s;
+    if (v->n_ins) { if ((s = upload(c, c->d_ins_off, v->off, (size_t)v->n_ins + 1))) return s; }
+    else if ((s = upload<uint64_t>(c, c->d_ins_off, nullptr, 0, 1))) return s;
+    if (nb) { if ((s = upload(c, c->d_ins_bases, v->bases, (size_t)nb))) return s; }
+    else if ((s = upload<uint8_t>(c, c->d_ins_bases, nullptr, 0, 1))) return s;
+    c->insseq_loaded = true;
+    return SVT_OK;
+}
+
+svt_status svt_poa_consensus(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, const svt_result *refined,
+                             size_t n, int32_t cap, uint8_t *bases, svt_poa_result *res) {
+    if (!c || !p) return SVT_EINVAL;
+    if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
+    if (!c->insseq_loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_insseq not called");
+    if (n == 0) return SVT_OK;
+    if (!loci || !refined || !res || cap < 0 || (cap > 0 && !bases)) return fail(c, SVT_EINVAL, "%s", "null arrays / cap");
+    if (n > 0x3fffffffull) return fail(c, SVT_EINVAL, "%s", "batch too large");
+    const int64_t w_max = (int64_t)p->band_b + (int64_t)p->band_f_permille * p->max_len / 1000;
+    if (p->match < 0 || p->mismatch < 0 || p->gap_open < 0 || p->gap_ext < 0 || p->band_b < 1 || p->band_f_permille < 0 ||
+        p->max_seqs < 1 || p->max_seqs > POA_PIN || p->max_len < 1 || p->max_len > POA_SEQ_MAX || w_max > 63 ||
+        p->max_nodes < p->max_len || p->max_nodes > 65000 || p->support_radius < 0 || p->max_support < 1 ||
+        p->match > 1000 || p->mismatch > 1000 || p->gap_open > 1000 || p->gap_ext > 1000)
+        return fail(c, SVT_EINVAL, "%s", "poa params out of range");
+    HIP_TRY(c, hipSetDevice(c->device));
+    svt_status s = poa_scratch(c, p, n);
+    if (s) return s;
+    return poa_run(c, p, loci, refined, n, cap, bases, res);
+}
+
 uint64_t svt_pileup_device_bytes(const svt_ctx *c) { return c ? c->dev_bytes : 0; }
 
 void svt_close(svt_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     free_pileup(c);
-    hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl);
+    hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->d_poa_slots);
     delete c;
 }
 

@@ -13,8 +13,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (LOCUS_DTYPE, RESULT_DTYPE, STATUS_NAMES, SW_QUERY_DTYPE, SW_WINDOW_DTYPE, SvtParams, SvtWork,
-                   load_engine, ptr)
+from ._lib import (LOCUS_DTYPE, POA_RESULT_DTYPE, RESULT_DTYPE, STATUS_NAMES, SW_QUERY_DTYPE, SW_WINDOW_DTYPE,
+                   SvtInsseqView, SvtParams, SvtPoaParams, SvtWork, load_engine, ptr)
 from .pileup import Pileup
 
 # params.h:27-32
@@ -111,6 +111,40 @@ class Engine:
         self._check(self.lib.svt_sliding_window_ins(self._h, ptr(q), len(q), int(window_size), int(slide_size),
                                                     ptr(best), ptr(sub)))
         return (best, off, sub) if with_subwindows else best
+
+    # ---- allele consensus (POA) of refined INS calls: no reference behaviour (the reference
+    # never calls abPOA); parity against oracle/poa_oracle.c only.  See include/svtrek_gpu.h.
+    @property
+    def ins_count(self) -> int:
+        """I >= 50 ops in the loaded pileup: the sequence count load_insseq expects."""
+        return int(self.lib.svt_pileup_ins_count(self._h))
+
+    def load_insseq(self, off: np.ndarray, bases: np.ndarray) -> None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        v = SvtInsseqView(len(off) - 1, ptr(off), ptr(bases) if len(bases) else None)
+        self._check(self.lib.svt_load_insseq(self._h, C.byref(v)))
+        self._insseq = (off, bases)
+
+    @staticmethod
+    def poa_params(**kw) -> SvtPoaParams:
+        p = SvtPoaParams()
+        load_engine().svt_poa_default_params(C.byref(p))
+        for k, v in kw.items():
+            setattr(p, k, int(v))
+        return p
+
+    def poa_consensus(self, loci: np.ndarray, refined: np.ndarray, cap: int = 4096, **kw):
+        """(POA_RESULT_DTYPE per locus, uint8 [n, cap] nt4 consensus bases)."""
+        loci = np.ascontiguousarray(loci, dtype=LOCUS_DTYPE)
+        refined = np.ascontiguousarray(refined, dtype=RESULT_DTYPE)
+        res = np.zeros(len(loci), dtype=POA_RESULT_DTYPE)
+        out = np.zeros((len(loci), cap), dtype=np.uint8)
+        p = self.poa_params(**kw)
+        if len(loci):
+            self._check(self.lib.svt_poa_consensus(self._h, C.byref(p), ptr(loci), ptr(refined), len(loci), cap,
+                                                   ptr(out), ptr(res)))
+        return res, out
 
     @property
     def device_bytes(self) -> int:

@@ -140,6 +140,29 @@ def generate(cfg: SimConfig, keep_handle: bool = False) -> SimResult:
     return SimResult(pile, loci, truth, hd if keep_handle else None)
 
 
+def insertion_sequences(res: SimResult, cfg: SimConfig, err_permille: int = 50) -> tuple[np.ndarray, np.ndarray]:
+    """(off uint64 [n+1], bases uint8 nt4) for every I >= 50 op of the pileup in (read, op)
+    order -- svt_load_insseq's input.  Ops carrying an INS locus get that locus's allele with
+    per-base substitutions (err_permille / 1000); others random bases.  Seeded by cfg.seed."""
+    if res.handle is None:
+        raise ValueError("generate(..., keep_handle=True) is required")
+    lib = load_sim()
+    n = C.c_uint64(0)
+    po, pb = C.c_void_p(), C.c_void_p()
+    if lib.sim_insseq(res.handle.h, cfg.seed, cfg.bp_jitter, err_permille, C.byref(n), C.byref(po), C.byref(pb)):
+        raise MemoryError("sim_insseq")
+    try:
+        nn = int(n.value)
+        off = np.frombuffer((C.c_char * (8 * (nn + 1))).from_address(po.value), dtype=np.uint64).copy()
+        nb = int(off[-1])
+        bases = (np.frombuffer((C.c_char * nb).from_address(pb.value), dtype=np.uint8).copy() if nb
+                 else np.zeros(0, dtype=np.uint8))
+    finally:
+        lib.sim_free_buf(po)
+        lib.sim_free_buf(pb)
+    return off, bases
+
+
 def write_bam(res: SimResult, path: str, with_seq: bool = False, level: int = 6) -> None:
     if res.handle is None:
         raise ValueError("generate(..., keep_handle=True) is required to write a BAM")

@@ -1,0 +1,124 @@
+"""GPU allele-consensus (POA) mode vs the CPU oracle (oracle/poa_oracle.c), bit-exact per
+locus: supporting sequences, sequences fused, consensus bases.  The reference never calls
+abPOA, so this mode is parity-unpinned by the reference (see test_poa_oracle.py)."""
+import numpy as np
+import oracle_ffi as O
+import pytest
+
+from svtrek_amd import SVT_NA, Params, SvtError, from_reads, make_loci, sim
+
+pytestmark = pytest.mark.gpu
+
+
+def ins_base_of(pl) -> np.ndarray:
+    """Per read: index of its first I >= 50 op in the pileup-wide (read, op) order."""
+    ins = ((pl.cigar & 15) == 1) & ((pl.cigar >> 4) >= 50)
+    c = np.concatenate([[0], np.cumsum(ins, dtype=np.int64)])
+    return c[pl.cig_off[:-1].astype(np.int64)].astype(np.uint64)
+
+
+def check(eng, pl, loci, off, bases, cap=4096, **kw):
+    refined = eng.refine(loci)
+    res, out = eng.poa_consensus(loci, refined, cap=cap, **kw)
+    ib = ins_base_of(pl)
+    prm = eng.params
+    pp = dict(O.POA_DEFAULTS)
+    pp.update(kw)
+    n_checked = 0
+    for i, l in enumerate(loci):
+        R = int(refined["start"][i])
+        if int(l["type"]) != 1 or R == SVT_NA:
+            assert res["len"][i] == -1
+            continue
+        s = (int(l["pos"]) - prm.median_interval) & 0xFFFFFFFF
+        e = (int(l["pos"]) + prm.median_interval) & 0xFFFFFFFF
+        idx = O.poa_support(pl, ib, int(l["chrom"]), s, e, R, cap=pp["max_support"], **kw)
+        seqs = [bases[off[k]:off[k + 1]] for k in idx]
+        want, used = O.poa_consensus(seqs, **kw)     # full length; the GPU writes min(len, cap)
+        assert res["n_used"][i] == used, (i, res[i], used)
+        assert res["len"][i] == len(want), (i, res[i], len(want))
+        assert np.array_equal(out[i, :min(len(want), cap)], want[:cap]), i
+        n_checked += 1
+    return n_checked, res
+
+
+def noisy_sub(rng, a, p):
+    s = a.copy()
+    m = rng.random(len(s)) < p
+    s[m] = (s[m] + rng.integers(1, 4, int(m.sum()))) & 3
+    return s
+
+
+def test_direct_clusters(engine_factory):
+    """INS clusters with known alleles: reads carry noisy copies (plus unrelated I >= 50 ops)."""
+    rng = np.random.default_rng(1)
+    rows, seqrows = [], []
+    loci_rows = []
+    for k in range(12):
+        c = 100000 + 40000 * k
+        L = int(rng.choice([50, 80, 300, 1200]))
+        allele = rng.integers(0, 4, L).astype(np.uint8)
+        for _ in range(int(rng.integers(3, 14))):
+            lead = 2000 + int(rng.integers(-500, 500))
+            pos = c + int(rng.integers(-3, 4)) - lead
+            s = noisy_sub(rng, allele, 0.05) if rng.random() < 0.85 else rng.integers(0, 4, L).astype(np.uint8)
+            ops = [(0, lead), (1, len(s)), (0, 3000)]
+            sq = [s]
+            if rng.random() < 0.2:   # an unrelated insertion later in the read
+                x = rng.integers(0, 4, 60).astype(np.uint8)
+                ops += [(1, 60), (0, 500)]
+                sq.append(x)
+            rows.append((0, pos, ops))
+            seqrows.append(sq)
+        loci_rows.append((1, 1, c + int(rng.integers(-30, 30)), c + 1))
+    order = sorted(range(len(rows)), key=lambda i: (rows[i][1], i))
+    rows = [rows[i] for i in order]
+    seqrows = [seqrows[i] for i in order]
+    pl = from_reads(1, rows)
+    flat = [s for sq in seqrows for s in sq]
+    off = np.concatenate([[0], np.cumsum([len(s) for s in flat])]).astype(np.uint64)
+    bases = np.concatenate(flat).astype(np.uint8)
+    eng = engine_factory(Params(consensus_min_count=2))
+    eng.load_pileup(pl)
+    assert eng.ins_count == len(flat)
+    eng.load_insseq(off, bases)
+    n, res = check(eng, pl, make_loci(loci_rows), off, bases)
+    assert n >= 8 and (res["n_used"] > 0).sum() >= 8
+
+
+def test_sim_workload(engine_factory):
+    cfg = sim.SimConfig(seed=21, n_targets=2, n_loci=60, del_frac=0.3, coverage=15, sv_max_len=1500,
+                        p_noise_sv=0.2)
+    r = sim.generate(cfg, keep_handle=True)
+    off, bases = sim.insertion_sequences(r, cfg, err_permille=60)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    eng.load_insseq(off, bases)
+    n, res = check(eng, r.pileup, r.loci, off, bases)
+    assert n >= 20
+
+
+def test_small_caps_and_params(engine_factory):
+    cfg = sim.SimConfig(seed=22, n_targets=1, n_loci=30, del_frac=0.0, coverage=20, sv_max_len=900)
+    r = sim.generate(cfg, keep_handle=True)
+    off, bases = sim.insertion_sequences(r, cfg, err_permille=80)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    eng.load_insseq(off, bases)
+    check(eng, r.pileup, r.loci, off, bases, cap=100, max_seqs=5, max_support=8, band_b=6, band_f_permille=20,
+          support_radius=8, max_nodes=1500, max_len=900)
+
+
+def test_insseq_validation(engine_factory):
+    cfg = sim.SimConfig(seed=23, n_targets=1, n_loci=5, del_frac=0.0, coverage=5)
+    r = sim.generate(cfg, keep_handle=True)
+    off, bases = sim.insertion_sequences(r, cfg)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    with pytest.raises(SvtError):   # before svt_load_insseq
+        eng.poa_consensus(r.loci, eng.refine(r.loci))
+    with pytest.raises(SvtError):   # wrong count
+        eng.load_insseq(off[:-1], bases)
+    eng.load_insseq(off, bases)
+    with pytest.raises(SvtError):   # band wider than 63
+        eng.poa_consensus(r.loci, eng.refine(r.loci), band_b=60)
