@@ -202,6 +202,9 @@ svt_status svt_load_insseq(svt_ctx *ctx, const svt_insseq_view *seqs);
 svt_status svt_poa_consensus(svt_ctx *ctx, const svt_poa_params *p, const svt_locus *loci,
                              const svt_result *refined, size_t n, int32_t cap, uint8_t *bases,
                              svt_poa_result *res);
+/* Loci the last svt_poa_consensus call reran on full-size scratch slots (their graphs
+ * outgrew the small slots' node budget); a diagnostic, results do not depend on it. */
+uint64_t   svt_poa_deferred(const svt_ctx *ctx);
 
 /* Bytes of device memory the loaded pileup occupies. */
 uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);

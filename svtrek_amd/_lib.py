@@ -82,6 +82,7 @@ ENGINE_SYMBOLS = (
     "svt_count_work", "svt_pileup_device_bytes", "svt_last_error", "svt_close", "svt_version",
     "svt_sw_subwindows", "svt_sliding_window_ins",
     "svt_poa_default_params", "svt_pileup_ins_count", "svt_load_insseq", "svt_poa_consensus",
+    "svt_poa_deferred",
 )
 
 _engine = None
@@ -124,6 +125,8 @@ def load_engine() -> C.CDLL:
     lib.svt_pileup_ins_count.restype = C.c_uint64
     lib.svt_load_insseq.argtypes = [P, C.POINTER(SvtInsseqView)]
     lib.svt_poa_consensus.argtypes = [P, C.POINTER(SvtPoaParams), P, P, C.c_size_t, C.c_int32, P, P]
+    lib.svt_poa_deferred.argtypes = [P]
+    lib.svt_poa_deferred.restype = C.c_uint64
     for name in ("svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
                  "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):
         getattr(lib, name).restype = C.c_int32

@@ -46,6 +46,18 @@ def build_engine(force: bool = False) -> str:
     return out
 
 
+def build_test_engine(force: bool = False) -> str:
+    """Test artefact: the engine with a 2-row POA ring (svt_poa.inc SVT_POA_RING), so nearly
+    every predecessor is read from a spill row -- tests/test_gpu_poa.py runs parity on it."""
+    out = os.path.join(PKG, "variants", "libsvtrek_hip_ring2.so")
+    deps = [os.path.join(CSRC, "svt_engine.hip"), os.path.join(INC, "svtrek_gpu.h"), os.path.join(CSRC, "svt_poa.inc")]
+    if force or _stale(out, deps):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DSVT_POA_RING=2",
+              "-I", INC, "-o", out, deps[0]])
+    return out
+
+
 def build_host(force: bool = False) -> str:
     out = os.path.join(PKG, "libsvtrek_host.so")
     srcs = [os.path.join(CSRC, f) for f in ("bam_ingest.cpp", "vcf_audit.cpp")]
@@ -89,6 +101,7 @@ def build_oracle(force: bool = False) -> str:
 def build_all(force: bool = False) -> dict[str, str]:
     arts = {
         "engine": build_engine(force),
+        "engine_ring2": build_test_engine(force),
         "sim": build_sim(force),
         "oracle": build_oracle(force),
     }

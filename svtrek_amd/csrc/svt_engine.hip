@@ -1566,9 +1566,8 @@ struct svt_ctx {
     uint64_t *d_ins_off = nullptr;
     uint8_t *d_ins_bases = nullptr;
     bool insseq_loaded = false;
-    uint8_t *d_poa_slots = nullptr;
-    uint64_t poa_slot_bytes = 0;
-    uint32_t poa_nslots = 0;
+    PoaPool poa_small, poa_big;       // POA scratch slots (poa_pool)
+    uint64_t poa_deferred = 0;        // loci the last svt_poa_consensus reran on full-size slots
     uint2 *d_ev = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
@@ -1678,19 +1677,67 @@ svt_status upload(svt_ctx *c, T *&dst, const T *src, size_t n, size_t pad_elems 
     return SVT_OK;
 }
 
-// POA scratch: one slot per persistent wave, min(batch, POA_SLOTS) slots, kept across calls.
-constexpr uint64_t POA_SLOTS = 256;
+// POA scratch, kept across calls: one slot per persistent wave in two pools.  The many
+// small slots hold graphs up to POA_SMALL_NODES nodes with POA_SMALL_SPILL spill rows (a
+// typical allele's graph is a few thousand nodes and spills none); loci that outgrow them
+// rerun on the few full-size slots.  Sizes at the default parameters: 1792 x 8.6 MB
+// (7 waves per CU: the LDS ring bounds occupancy) and 256 x 50 MB.
+constexpr uint64_t POA_SLOTS_SMALL = 1792;
+constexpr uint64_t POA_SLOTS_BIG = 256;
+constexpr int32_t POA_SMALL_NODES = 16384;
+constexpr int32_t POA_SMALL_SPILL = 256;
 
-svt_status poa_scratch(svt_ctx *c, const svt_poa_params *p, size_t n) {
-    const uint64_t sb = poa_slot_bytes(p->max_nodes, p->max_len, p->max_support);
-    const uint64_t want = std::min<uint64_t>(n, POA_SLOTS);
-    if (c->d_poa_slots && c->poa_slot_bytes == sb && c->poa_nslots >= want) return SVT_OK;
-    hfree(c->d_poa_slots);
-    c->poa_nslots = 0;
-    if (hipMalloc(&c->d_poa_slots, want * sb) != hipSuccess)
+svt_status poa_pool(svt_ctx *c, PoaPool &pl, int32_t node_cap, int32_t spill_cap, const svt_poa_params *p,
+                    uint64_t want) {
+    const uint64_t sb = poa_slot_bytes(node_cap, spill_cap, p->max_len, p->max_support);
+    if (pl.d && pl.slot_bytes == sb && pl.nslots >= want) return SVT_OK;
+    hfree(pl.d);
+    pl.nslots = 0;
+    if (hipMalloc(&pl.d, want * sb) != hipSuccess) {
+        pl.d = nullptr;
         return fail(c, SVT_ENOMEM, "%s", "poa scratch (lower max_nodes / max_len)");
-    c->poa_slot_bytes = sb;
-    c->poa_nslots = (uint32_t)want;
+    }
+    pl.slot_bytes = sb;
+    pl.nslots = (uint32_t)want;
+    return SVT_OK;
+}
+
+// SVTREK_POA_SMALL_NODES overrides the small slots' node budget (tests force deferral).
+int32_t poa_small_cap(const svt_poa_params *p) {
+    const char *ev = getenv("SVTREK_POA_SMALL_NODES");
+    const int32_t want = ev ? (int32_t)atoi(ev) : POA_SMALL_NODES;
+    return std::min(p->max_nodes, std::max(want, p->max_len + 2));
+}
+
+// One persistent launch of poa_kernel over d_list (or all n loci) on pool pl; synchronous.
+svt_status poa_launch(svt_ctx *c, PoaArgs a, const PoaPool &pl, int32_t node_cap, int32_t spill_cap,
+                      const uint32_t *d_list, uint32_t n, uint32_t *d_queue) {
+    a.slots = pl.d;
+    a.slot_bytes = pl.slot_bytes;
+    a.node_cap = node_cap;
+    a.spill_cap = spill_cap;
+    a.list = d_list;
+    a.n = n;
+    a.queue = d_queue;
+    a.diag = nullptr;
+    HIP_TRY(c, hipMemset(d_queue, 0, sizeof(uint32_t)));
+#if SVT_POA_DIAG
+    HIP_TRY(c, hipMalloc(&a.diag, PD_N * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemset(a.diag, 0, PD_N * sizeof(unsigned long long)));
+#endif
+    const unsigned grid = (unsigned)std::min<uint64_t>(pl.nslots, n);
+    hipLaunchKernelGGL(poa_kernel, dim3(grid), dim3(64), 0, nullptr, a);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipDeviceSynchronize());
+#if SVT_POA_DIAG
+    unsigned long long h[PD_N];
+    HIP_TRY(c, hipMemcpy(h, a.diag, sizeof h, hipMemcpyDeviceToHost));
+    (void)hipFree(a.diag);
+    fprintf(stderr, "poa_diag node_cap=%d grid=%u loci=%u wave-ms: support %.1f load %.1f rows %.1f trace %.1f "
+            "fuse %.1f cons %.1f | rows %llu steps %llu seqs %llu far %llu\n", node_cap, grid, n, h[PD_SUPPORT] * 1e-5,
+            h[PD_LOAD] * 1e-5, h[PD_ROWS] * 1e-5, h[PD_TRACE] * 1e-5, h[PD_FUSE] * 1e-5, h[PD_CONS] * 1e-5,
+            h[PD_NROWS], h[PD_NSTEPS], h[PD_NSEQ], h[PD_NFAR]);
+#endif
     return SVT_OK;
 }
 
@@ -1700,15 +1747,18 @@ svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, c
     svt_result *d_ref = nullptr;
     uint8_t *d_out = nullptr;
     int4 *d_res = nullptr;
+    uint32_t *d_aux = nullptr;   // [0] work queue, [1 ..] deferred loci
     svt_status s = SVT_OK;
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && s == SVT_OK) s = fail(c, SVT_EDEVICE, what, hipGetErrorString(e));
         return s == SVT_OK;
     };
+    const int32_t small_cap = poa_small_cap(p);
     if (chk(hipMalloc(&d_loci, n * sizeof(svt_locus)), "hipMalloc: %s") &&
         chk(hipMalloc(&d_ref, n * sizeof(svt_result)), "hipMalloc: %s") &&
         chk(hipMalloc(&d_out, std::max<size_t>(1, n * (size_t)cap)), "hipMalloc: %s") &&
         chk(hipMalloc(&d_res, n * sizeof(int4)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_aux, (n + 1) * sizeof(uint32_t)), "hipMalloc: %s") &&
         chk(hipMemcpy(d_loci, loci, n * sizeof(svt_locus), hipMemcpyHostToDevice), "H2D: %s") &&
         chk(hipMemcpy(d_ref, refined, n * sizeof(svt_result), hipMemcpyHostToDevice), "H2D: %s")) {
         const KArgs k = make_args(c, nullptr, nullptr, 0, false);
@@ -1719,22 +1769,31 @@ svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, c
                          p->max_seqs, p->max_len, p->max_nodes, p->support_radius, p->max_support};
         a.loci = d_loci;
         a.refined = d_ref;
-        a.n = (uint32_t)n;
         a.ins_base = c->d_insbase;
         a.ins_off = c->d_ins_off;
         a.ins_bases = c->d_ins_bases;
-        a.slots = c->d_poa_slots;
-        a.slot_bytes = c->poa_slot_bytes;
         a.cap = cap;
         a.out = d_out;
         a.res = d_res;
-        const unsigned grid = (unsigned)std::min<uint64_t>(c->poa_nslots, n);
-        hipLaunchKernelGGL(poa_kernel, dim3(grid), dim3(64), 0, nullptr, a);
-        if (chk(hipGetLastError(), "poa_kernel: %s") && chk(hipDeviceSynchronize(), "poa_kernel: %s") &&
-            chk(hipMemcpy(res, d_res, n * sizeof(int4), hipMemcpyDeviceToHost), "D2H: %s") && cap > 0)
-            chk(hipMemcpy(bases, d_out, n * (size_t)cap, hipMemcpyDeviceToHost), "D2H: %s");
+        if (s == SVT_OK)
+            s = poa_pool(c, c->poa_small, small_cap, POA_SMALL_SPILL, p, std::min<uint64_t>(n, POA_SLOTS_SMALL));
+        if (s == SVT_OK) s = poa_launch(c, a, c->poa_small, small_cap, POA_SMALL_SPILL, nullptr, (uint32_t)n, d_aux);
+        if (chk(hipMemcpy(res, d_res, n * sizeof(int4), hipMemcpyDeviceToHost), "D2H: %s")) {
+            std::vector<uint32_t> deferred;
+            for (size_t i = 0; i < n; i++)
+                if (res[i].status == POA_DEFER) deferred.push_back((uint32_t)i);
+            if (!deferred.empty()) {
+                const uint32_t nd = (uint32_t)deferred.size();
+                if (chk(hipMemcpy(d_aux + 1, deferred.data(), nd * sizeof(uint32_t), hipMemcpyHostToDevice), "H2D: %s"))
+                    s = poa_pool(c, c->poa_big, p->max_nodes, p->max_nodes + 2, p, std::min<uint64_t>(nd, POA_SLOTS_BIG));
+                if (s == SVT_OK) s = poa_launch(c, a, c->poa_big, p->max_nodes, p->max_nodes + 2, d_aux + 1, nd, d_aux);
+                if (s == SVT_OK) chk(hipMemcpy(res, d_res, n * sizeof(int4), hipMemcpyDeviceToHost), "D2H: %s");
+            }
+            c->poa_deferred = deferred.size();
+            if (s == SVT_OK && cap > 0) chk(hipMemcpy(bases, d_out, n * (size_t)cap, hipMemcpyDeviceToHost), "D2H: %s");
+        }
     }
-    hfree(d_loci); hfree(d_ref); hfree(d_out); hfree(d_res);
+    hfree(d_loci); hfree(d_ref); hfree(d_out); hfree(d_res); hfree(d_aux);
     return s;
 }
 
@@ -2095,18 +2154,18 @@ svt_status svt_poa_consensus(svt_ctx *c, const svt_poa_params *p, const svt_locu
         p->match > 1000 || p->mismatch > 1000 || p->gap_open > 1000 || p->gap_ext > 1000)
         return fail(c, SVT_EINVAL, "%s", "poa params out of range");
     HIP_TRY(c, hipSetDevice(c->device));
-    svt_status s = poa_scratch(c, p, n);
-    if (s) return s;
     return poa_run(c, p, loci, refined, n, cap, bases, res);
 }
 
 uint64_t svt_pileup_device_bytes(const svt_ctx *c) { return c ? c->dev_bytes : 0; }
 
+uint64_t svt_poa_deferred(const svt_ctx *c) { return c ? c->poa_deferred : 0; }
+
 void svt_close(svt_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     free_pileup(c);
-    hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->d_poa_slots);
+    hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->poa_small.d); hfree(c->poa_big.d);
     delete c;
 }
 

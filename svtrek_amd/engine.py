@@ -147,6 +147,11 @@ class Engine:
         return res, out
 
     @property
+    def poa_deferred(self) -> int:
+        """Loci the last poa_consensus call reran on full-size scratch slots."""
+        return int(self.lib.svt_poa_deferred(self._h))
+
+    @property
     def device_bytes(self) -> int:
         return int(self.lib.svt_pileup_device_bytes(self._h))
 

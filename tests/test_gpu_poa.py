@@ -1,6 +1,10 @@
 """GPU allele-consensus (POA) mode vs the CPU oracle (oracle/poa_oracle.c), bit-exact per
 locus: supporting sequences, sequences fused, consensus bases.  The reference never calls
 abPOA, so this mode is parity-unpinned by the reference (see test_poa_oracle.py)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import oracle_ffi as O
 import pytest
@@ -122,3 +126,40 @@ def test_insseq_validation(engine_factory):
     eng.load_insseq(off, bases)
     with pytest.raises(SvtError):   # band wider than 63
         eng.poa_consensus(r.loci, eng.refine(r.loci), band_b=60)
+
+
+def test_deferred_loci_rerun_on_full_slots(engine_factory, monkeypatch):
+    """Graphs that outgrow the small scratch slots rerun on full-size ones; results unchanged."""
+    cfg = sim.SimConfig(seed=24, n_targets=1, n_loci=40, del_frac=0.0, coverage=15, sv_min_len=200,
+                        sv_max_len=1500)
+    r = sim.generate(cfg, keep_handle=True)
+    off, bases = sim.insertion_sequences(r, cfg, err_permille=60)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    eng.load_insseq(off, bases)
+    monkeypatch.setenv("SVTREK_POA_SMALL_NODES", "1")    # budget = max_len + 2 nodes
+    n, res = check(eng, r.pileup, r.loci, off, bases, max_len=1500)
+    assert n >= 10
+    assert eng.poa_deferred >= 5
+    assert (res["status"] == 0).all()
+    monkeypatch.delenv("SVTREK_POA_SMALL_NODES")
+    res2, _ = eng.poa_consensus(r.loci, eng.refine(r.loci), max_len=1500)
+    if not os.environ.get("SVTREK_POA_SUBRUN"):   # the ring-2 build also defers on spill overflow
+        assert eng.poa_deferred == 0
+    assert np.array_equal(res, res2)
+
+
+def test_spill_rows_ring2_build():
+    """The POA parity tests above, rerun on the engine built with a 2-row LDS ring
+    (svtrek_amd/variants/libsvtrek_hip_ring2.so): nearly every predecessor row then comes from
+    a spill row, and small slots defer on spill overflow.  One child process."""
+    if os.environ.get("SVTREK_POA_SUBRUN"):
+        pytest.skip("already the ring-2 run")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "svtrek_amd", "variants", "libsvtrek_hip_ring2.so")
+    assert os.path.exists(lib), "ring-2 test engine not built (python svtrek_amd/build.py)"
+    env = dict(os.environ, SVTREK_ENGINE_LIB=lib, SVTREK_POA_SUBRUN="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.abspath(__file__), "-x", "-q", "-m", "gpu",
+                        "-p", "no:cacheprovider", "--timeout", "240", "--timeout-method", "thread"],
+                       env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]

@@ -93,7 +93,7 @@ def main() -> None:
         "metric": "INS allele consensus loci/sec (POA mode, 1 GPU)",
         "value": round(len(ins) / gpu_s, 1), "unit": "loci/s",
         "workload": a.workload, "ins_loci": int(len(ins)), "refined_ins": n_ref, "consensus_loci": int(done.sum()),
-        "sequences_fused": fused, "gpu_s": round(gpu_s, 4), "gpu_s_all": [round(x, 4) for x in times],
+        "sequences_fused": fused, "deferred_to_full_slots": eng.poa_deferred, "gpu_s": round(gpu_s, 4), "gpu_s_all": [round(x, 4) for x in times],
         "timing": "svt_poa_consensus wall time incl. H2D of loci/results and D2H of consensus bases",
         "parity_checked": int(min(a.check, len(idx_done))), "parity_mismatches": mism,
         "cpu_baseline": {"value": round(cpu_rate, 2) if cpu_rate else None, "unit": "loci/s", "cores": 1,
