@@ -1689,7 +1689,7 @@ constexpr int32_t POA_SMALL_SPILL = 256;
 
 svt_status poa_pool(svt_ctx *c, PoaPool &pl, int32_t node_cap, int32_t spill_cap, const svt_poa_params *p,
                     uint64_t want) {
-    const uint64_t sb = poa_slot_bytes(node_cap, spill_cap, p->max_len, p->max_support);
+    const uint64_t sb = poa_slot_bytes(node_cap, spill_cap, p->max_len);
     if (pl.d && pl.slot_bytes == sb && pl.nslots >= want) return SVT_OK;
     hfree(pl.d);
     pl.nslots = 0;
@@ -1724,6 +1724,7 @@ svt_status poa_launch(svt_ctx *c, PoaArgs a, const PoaPool &pl, int32_t node_cap
 #if SVT_POA_DIAG
     HIP_TRY(c, hipMalloc(&a.diag, PD_N * sizeof(unsigned long long)));
     HIP_TRY(c, hipMemset(a.diag, 0, PD_N * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemset(a.diag + PD_T0, 0xff, sizeof(unsigned long long)));
 #endif
     const unsigned grid = (unsigned)std::min<uint64_t>(pl.nslots, n);
     hipLaunchKernelGGL(poa_kernel, dim3(grid), dim3(64), 0, nullptr, a);
@@ -1737,6 +1738,8 @@ svt_status poa_launch(svt_ctx *c, PoaArgs a, const PoaPool &pl, int32_t node_cap
             "fuse %.1f cons %.1f | rows %llu steps %llu seqs %llu far %llu\n", node_cap, grid, n, h[PD_SUPPORT] * 1e-5,
             h[PD_LOAD] * 1e-5, h[PD_ROWS] * 1e-5, h[PD_TRACE] * 1e-5, h[PD_FUSE] * 1e-5, h[PD_CONS] * 1e-5,
             h[PD_NROWS], h[PD_NSTEPS], h[PD_NSEQ], h[PD_NFAR]);
+    fprintf(stderr, "poa_diag span %.1f ms, longest locus %.1f ms, busiest wave %.1f ms\n",
+            (h[PD_T1] - h[PD_T0]) * 1e-5, h[PD_LOCMAX] * 1e-5, h[PD_WAVEMAX] * 1e-5);
 #endif
     return SVT_OK;
 }
@@ -1747,7 +1750,8 @@ svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, c
     svt_result *d_ref = nullptr;
     uint8_t *d_out = nullptr;
     int4 *d_res = nullptr;
-    uint32_t *d_aux = nullptr;   // [0] work queue, [1 ..] deferred loci
+    uint32_t *d_aux = nullptr;   // [0] work queue, [1 .. n] locus order, [n+1 .. 2n] cost estimates
+    int32_t *d_sup = nullptr;    // [n] supporting sequences found, then [n][max_support] their indices
     svt_status s = SVT_OK;
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && s == SVT_OK) s = fail(c, SVT_EDEVICE, what, hipGetErrorString(e));
@@ -1758,7 +1762,8 @@ svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, c
         chk(hipMalloc(&d_ref, n * sizeof(svt_result)), "hipMalloc: %s") &&
         chk(hipMalloc(&d_out, std::max<size_t>(1, n * (size_t)cap)), "hipMalloc: %s") &&
         chk(hipMalloc(&d_res, n * sizeof(int4)), "hipMalloc: %s") &&
-        chk(hipMalloc(&d_aux, (n + 1) * sizeof(uint32_t)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_aux, (2 * n + 1) * sizeof(uint32_t)), "hipMalloc: %s") &&
+        chk(hipMalloc(&d_sup, n * (1 + (size_t)p->max_support) * sizeof(int32_t)), "hipMalloc: %s") &&
         chk(hipMemcpy(d_loci, loci, n * sizeof(svt_locus), hipMemcpyHostToDevice), "H2D: %s") &&
         chk(hipMemcpy(d_ref, refined, n * sizeof(svt_result), hipMemcpyHostToDevice), "H2D: %s")) {
         const KArgs k = make_args(c, nullptr, nullptr, 0, false);
@@ -1769,19 +1774,33 @@ svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, c
                          p->max_seqs, p->max_len, p->max_nodes, p->support_radius, p->max_support};
         a.loci = d_loci;
         a.refined = d_ref;
+        a.n = (uint32_t)n;
         a.ins_base = c->d_insbase;
         a.ins_off = c->d_ins_off;
         a.ins_bases = c->d_ins_bases;
         a.cap = cap;
         a.out = d_out;
         a.res = d_res;
+        a.nsupg = d_sup;
+        a.supg = d_sup + n;
+        a.est = d_aux + 1 + n;
+        a.diag = nullptr;
+        // supports + cost estimates, then the loci longest first (ties: input order)
+        hipLaunchKernelGGL(poa_support_kernel, dim3((unsigned)std::min<size_t>(n, 8192)), dim3(64), 0, nullptr, a);
+        std::vector<uint32_t> est(n), order(n);
+        if (chk(hipGetLastError(), "poa_support_kernel: %s") &&
+            chk(hipMemcpy(est.data(), a.est, n * sizeof(uint32_t), hipMemcpyDeviceToHost), "D2H: %s")) {
+            for (size_t i = 0; i < n; i++) order[i] = (uint32_t)i;
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return est[x] > est[y]; });
+            chk(hipMemcpy(d_aux + 1, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice), "H2D: %s");
+        }
         if (s == SVT_OK)
             s = poa_pool(c, c->poa_small, small_cap, POA_SMALL_SPILL, p, std::min<uint64_t>(n, POA_SLOTS_SMALL));
-        if (s == SVT_OK) s = poa_launch(c, a, c->poa_small, small_cap, POA_SMALL_SPILL, nullptr, (uint32_t)n, d_aux);
-        if (chk(hipMemcpy(res, d_res, n * sizeof(int4), hipMemcpyDeviceToHost), "D2H: %s")) {
-            std::vector<uint32_t> deferred;
-            for (size_t i = 0; i < n; i++)
-                if (res[i].status == POA_DEFER) deferred.push_back((uint32_t)i);
+        if (s == SVT_OK) s = poa_launch(c, a, c->poa_small, small_cap, POA_SMALL_SPILL, d_aux + 1, (uint32_t)n, d_aux);
+        if (s == SVT_OK && chk(hipMemcpy(res, d_res, n * sizeof(int4), hipMemcpyDeviceToHost), "D2H: %s")) {
+            std::vector<uint32_t> deferred;   // in the same longest-first order
+            for (size_t q = 0; q < n; q++)
+                if (res[order[q]].status == POA_DEFER) deferred.push_back(order[q]);
             if (!deferred.empty()) {
                 const uint32_t nd = (uint32_t)deferred.size();
                 if (chk(hipMemcpy(d_aux + 1, deferred.data(), nd * sizeof(uint32_t), hipMemcpyHostToDevice), "H2D: %s"))
@@ -1793,7 +1812,7 @@ svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, c
             if (s == SVT_OK && cap > 0) chk(hipMemcpy(bases, d_out, n * (size_t)cap, hipMemcpyDeviceToHost), "D2H: %s");
         }
     }
-    hfree(d_loci); hfree(d_ref); hfree(d_out); hfree(d_res); hfree(d_aux);
+    hfree(d_loci); hfree(d_ref); hfree(d_out); hfree(d_res); hfree(d_aux); hfree(d_sup);
     return s;
 }
 

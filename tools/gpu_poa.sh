@@ -15,5 +15,5 @@ cat "$OUT/bench.json"
 if [ -f svtrek_amd/variants/poa_diag.so ]; then
   SVTREK_ENGINE_LIB=$PWD/svtrek_amd/variants/poa_diag.so timeout -k 10 400 python tools/bench_poa.py --repeat 1 \
     --cpu-sample 1 --check 3 "$@" > "$OUT/diag.json" 2> "$OUT/diag.err" || { tail -5 "$OUT/diag.err"; exit 1; }
-  grep poa_diag "$OUT/diag.err" | tail -2
+  grep poa_diag "$OUT/diag.err" | tail -4
 fi
