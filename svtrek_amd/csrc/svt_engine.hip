@@ -1680,9 +1680,12 @@ svt_status upload(svt_ctx *c, T *&dst, const T *src, size_t n, size_t pad_elems 
 // POA scratch, kept across calls: one slot per persistent wave in two pools.  The many
 // small slots hold graphs up to POA_SMALL_NODES nodes with POA_SMALL_SPILL spill rows (a
 // typical allele's graph is a few thousand nodes and spills none); loci that outgrow them
-// rerun on the few full-size slots.  Sizes at the default parameters: 1792 x 8.6 MB
-// (7 waves per CU: the LDS ring bounds occupancy) and 256 x 50 MB.
-constexpr uint64_t POA_SLOTS_SMALL = 1792;
+// rerun on the few full-size slots.  Sizes at the default parameters: 2560 x 8.6 MB
+// (10 waves per CU: the LDS ring bounds occupancy at 11) and 256 x 50 MB.
+#ifndef SVT_POA_SLOTS_SMALL
+#define SVT_POA_SLOTS_SMALL 2560
+#endif
+constexpr uint64_t POA_SLOTS_SMALL = SVT_POA_SLOTS_SMALL;
 constexpr uint64_t POA_SLOTS_BIG = 256;
 constexpr int32_t POA_SMALL_NODES = 16384;
 constexpr int32_t POA_SMALL_SPILL = 256;

@@ -163,3 +163,17 @@ def test_spill_rows_ring2_build():
                         "-p", "no:cacheprovider", "--timeout", "240", "--timeout-method", "thread"],
                        env=env, cwd=root, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+
+
+def test_long_alleles_two_cells_per_lane(engine_factory):
+    """Alleles over 2100 bp: the band (2w + 1 columns) exceeds the wave, two cells per lane."""
+    cfg = sim.SimConfig(seed=25, n_targets=1, n_loci=12, del_frac=0.0, coverage=10, sv_min_len=2300,
+                        sv_max_len=3800)
+    r = sim.generate(cfg, keep_handle=True)
+    off, bases = sim.insertion_sequences(r, cfg, err_permille=50)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    eng.load_insseq(off, bases)
+    n, res = check(eng, r.pileup, r.loci, off, bases)
+    assert n >= 5
+    assert (res["len"][res["len"] > 0] > 2100).sum() >= 5
