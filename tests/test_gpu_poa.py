@@ -177,3 +177,39 @@ def test_long_alleles_two_cells_per_lane(engine_factory):
     n, res = check(eng, r.pileup, r.loci, off, bases)
     assert n >= 5
     assert (res["len"][res["len"] > 0] > 2100).sum() >= 5
+
+
+def test_edge_cases(engine_factory):
+    """N bases (code 4 never matches), one-sequence loci (consensus = the sequence), loci
+    whose supports all exceed max_len (n_used 0), cap 0, max_seqs 1."""
+    rng = np.random.default_rng(7)
+    rows, seqs, loci_rows = [], [], []
+    for k in range(10):
+        c = 200000 + 50000 * k
+        L = [60, 120, 700, 1000, 90, 400, 75, 2000, 55, 300][k]
+        allele = rng.integers(0, 5, L).astype(np.uint8)          # includes N (4)
+        n = 1 if k in (1, 4) else int(rng.integers(2, 9))
+        for _ in range(n):
+            lead = 1500 + int(rng.integers(-200, 200))
+            s = noisy_sub(rng, allele, 0.04)
+            s[rng.random(L) < 0.02] = 4
+            rows.append((0, c - lead + int(rng.integers(-2, 3)), [(0, lead), (1, L), (0, 2500)]))
+            seqs.append(s)
+        loci_rows.append((1, 1, c + int(rng.integers(-20, 20)), c + 1))
+    order = sorted(range(len(rows)), key=lambda i: (rows[i][1], i))
+    rows = [rows[i] for i in order]
+    seqs = [seqs[i] for i in order]
+    pl = from_reads(1, rows)
+    off = np.concatenate([[0], np.cumsum([len(s) for s in seqs])]).astype(np.uint64)
+    bases = np.concatenate(seqs).astype(np.uint8)
+    eng = engine_factory(Params(consensus_min_count=1))
+    eng.load_pileup(pl)
+    eng.load_insseq(off, bases)
+    loci = make_loci(loci_rows)
+    n, res = check(eng, pl, loci, off, bases)
+    assert n >= 8 and (res["n_used"] == 1).sum() >= 1
+    n, res = check(eng, pl, loci, off, bases, max_len=500)        # long alleles: no support
+    assert (res["len"] == 0).sum() >= 1
+    check(eng, pl, loci, off, bases, cap=0)
+    n, res = check(eng, pl, loci, off, bases, max_seqs=1)
+    assert res["n_used"].max() <= 1
