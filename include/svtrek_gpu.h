@@ -209,6 +209,18 @@ uint64_t   svt_poa_deferred(const svt_ctx *ctx);
 /* Bytes of device memory the loaded pileup occupies. */
 uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
 
+/* Where the last svt_load_pileup spent its time.  The device index (padded CIGAR arena,
+ * chunk index, walk ends, candidate-op lists) depends only on the pileup, like the BAI
+ * the reference's sam_itr_queryi needs (audit.c:271); it is built once per pileup and
+ * reported here so that per-query throughput can be quoted with and without it. */
+typedef struct svt_load_stats {
+    double host_ms;      /* host pass: validation, prefix-max endpos, records, buckets          */
+    double upload_ms;    /* synchronous H2D copies of the caller's arrays (CIGAR words incl.)    */
+    double index_ms;     /* device index build: pack_kernel + event_kernel (HIP events)          */
+    double total_ms;     /* wall time of the whole svt_load_pileup call                          */
+} svt_load_stats;
+svt_status svt_last_load_stats(const svt_ctx *ctx, svt_load_stats *out);
+
 const char *svt_last_error(const svt_ctx *ctx);
 void        svt_close(svt_ctx *ctx);
 const char *svt_version(void);

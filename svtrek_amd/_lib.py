@@ -76,13 +76,22 @@ class SvtWork(C.Structure):
     ]
 
 
+class SvtLoadStats(C.Structure):
+    _fields_ = [
+        ("host_ms", C.c_double),
+        ("upload_ms", C.c_double),
+        ("index_ms", C.c_double),
+        ("total_ms", C.c_double),
+    ]
+
+
 # every symbol include/svtrek_gpu.h declares
 ENGINE_SYMBOLS = (
     "svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
     "svt_count_work", "svt_pileup_device_bytes", "svt_last_error", "svt_close", "svt_version",
     "svt_sw_subwindows", "svt_sliding_window_ins",
     "svt_poa_default_params", "svt_pileup_ins_count", "svt_load_insseq", "svt_poa_consensus",
-    "svt_poa_deferred",
+    "svt_poa_deferred", "svt_last_load_stats",
 )
 
 _engine = None
@@ -116,6 +125,7 @@ def load_engine() -> C.CDLL:
     lib.svt_close.argtypes = [P]
     lib.svt_close.restype = None
     lib.svt_version.restype = C.c_char_p
+    lib.svt_last_load_stats.argtypes = [P, C.POINTER(SvtLoadStats)]
     lib.svt_sw_subwindows.argtypes = [P, C.c_int32]
     lib.svt_sw_subwindows.restype = C.c_uint64
     lib.svt_sliding_window_ins.argtypes = [P, P, C.c_size_t, C.c_int32, C.c_int32, P, P]

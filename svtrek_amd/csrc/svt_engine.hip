@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <vector>
 
@@ -1571,6 +1572,7 @@ struct svt_ctx {
     uint2 *d_ev = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
+    svt_load_stats load_stats{};      // timings of the last svt_load_pileup
     // batch scratch
     svt_locus *d_loci = nullptr;
     svt_result *d_out = nullptr;
@@ -1869,6 +1871,10 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
         return fail(c, SVT_EINVAL, "pileup: %s", "bad n_targets / tid_off");
     HIP_TRY(c, hipSetDevice(c->device));
     free_pileup(c);
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    const clk::time_point t_start = clk::now();
+    c->load_stats = svt_load_stats{};
     const int32_t nt = p->n_targets;
     const int64_t nr = nt ? p->tid_off[nt] : 0;
     if (nt && p->tid_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "tid_off[0] != 0");
@@ -1928,6 +1934,8 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     }
     poff[(size_t)nr] = pw;
     bkt_off[(size_t)nt] = (int64_t)bkt.size();
+    c->load_stats.host_ms = ms_since(t_start);
+    const clk::time_point t_up = clk::now();
     svt_status s;
     if ((s = upload(c, c->d_pos, p->pos, (size_t)nr))) return s;
     if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
@@ -1956,11 +1964,16 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
         if (e == hipSuccess) e = hipMalloc(&c->d_evoff, ((size_t)nr + 1) * 8);
         if (e == hipSuccess && nops) e = hipMemcpy(d_raw, p->cigar, nops * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
+        c->load_stats.upload_ms = ms_since(t_up);
+        hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
+        if (e == hipSuccess) e = hipEventRecord(ev[0], nullptr);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, d_raw, d_raw_off,
                                c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, c->d_rec2, d_nev, (int64_t)nr);
             e = hipGetLastError();
         }
+        if (e == hipSuccess) e = hipEventRecord(ev[1], nullptr);
         if (e == hipSuccess) e = hipMemcpy(nev.data(), d_nev, (size_t)nr * 8, hipMemcpyDeviceToHost);
         hfree(d_raw);
         hfree(d_raw_off);
@@ -1984,11 +1997,23 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
         if (e == hipSuccess) e = hipMalloc(&c->d_ev, std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2));
         if (e == hipSuccess) {
             c->dev_bytes += std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2);
-            hipLaunchKernelGGL(event_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
-                               c->d_off64, c->d_rec, c->d_rec2, c->d_evoff, c->d_ev, (int64_t)nr);
-            e = hipGetLastError();
+            e = hipEventRecord(ev[2], nullptr);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(event_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
+                                   c->d_off64, c->d_rec, c->d_rec2, c->d_evoff, c->d_ev, (int64_t)nr);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipEventRecord(ev[3], nullptr);
         }
         if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e == hipSuccess) {
+            float a = 0.f, b = 0.f;
+            e = hipEventElapsedTime(&a, ev[0], ev[1]);
+            if (e == hipSuccess) e = hipEventElapsedTime(&b, ev[2], ev[3]);
+            c->load_stats.index_ms = (double)a + (double)b;
+        }
+        for (int k = 0; k < 4; k++)
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
         if (e != hipSuccess) return fail(c, SVT_EDEVICE, "pileup pack: %s", hipGetErrorString(e));
     } else {
         if ((s = upload<uint2>(c, c->d_ev, nullptr, 0, 1))) return s;
@@ -1998,6 +2023,14 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     c->n_reads = nr;
     c->n_ops = nops;
     c->loaded = true;
+    if (nr == 0) c->load_stats.upload_ms = ms_since(t_up);
+    c->load_stats.total_ms = ms_since(t_start);
+    return SVT_OK;
+}
+
+svt_status svt_last_load_stats(const svt_ctx *c, svt_load_stats *out) {
+    if (!c || !out) return SVT_EINVAL;
+    *out = c->load_stats;
     return SVT_OK;
 }
 

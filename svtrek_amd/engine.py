@@ -14,7 +14,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from ._lib import (LOCUS_DTYPE, POA_RESULT_DTYPE, RESULT_DTYPE, STATUS_NAMES, SW_QUERY_DTYPE, SW_WINDOW_DTYPE,
-                   SvtInsseqView, SvtParams, SvtPoaParams, SvtWork, load_engine, ptr)
+                   SvtInsseqView, SvtLoadStats, SvtParams, SvtPoaParams, SvtWork, load_engine, ptr)
 from .pileup import Pileup
 
 # params.h:27-32
@@ -154,6 +154,12 @@ class Engine:
     @property
     def device_bytes(self) -> int:
         return int(self.lib.svt_pileup_device_bytes(self._h))
+
+    def load_stats(self) -> dict:
+        """Timings (ms) of the last load_pileup: host pass, H2D copies, device index build."""
+        st = SvtLoadStats()
+        self._check(self.lib.svt_last_load_stats(self._h, C.byref(st)))
+        return {k: round(getattr(st, k), 3) for k, _ in SvtLoadStats._fields_}
 
     def close(self) -> None:
         if getattr(self, "_h", None):
