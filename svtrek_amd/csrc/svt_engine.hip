@@ -36,7 +36,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.3 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.4 (gfx950, event walk)"
 
 namespace {
 
@@ -1479,7 +1479,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
     uint32_t carry = rpos, nev = 0, nins = 0;
     // PK_U 64-op steps per pass: their words are loaded up front (PK_U loads in flight per
     // wave instead of one), then scanned in order
-    constexpr int PK_U = 4;
+    constexpr int PK_U = 8;
     for (uint64_t b0 = 0; b0 < npad; b0 += PK_U * WAVE) {
         uint32_t wv[PK_U];
 #pragma unroll
