@@ -1079,6 +1079,42 @@ __device__ __forceinline__ void wave_bitonic_sort(int32_t *buf, int N) {
     }
 }
 
+// x of lane ln ^ J without an LDS round trip: DPP quad permutes (1, 2), row shifts (4), row
+// rotate (8), and gfx950's permlane swaps (16, 32).  A swap of x with itself yields the two
+// halves {[lo, lo], [hi, hi]} (rows for 16); whichever of them does not hold this lane's own
+// value at this lane holds the partner's (and if both do, the two values are equal).
+template <int J>
+__device__ __forceinline__ int32_t lane_xor(int32_t x) {
+    if constexpr (J == 1) {
+        return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    } else if constexpr (J == 4) {
+        const int32_t up = __builtin_amdgcn_update_dpp(0, x, 0x104, 0xf, 0xf, false);   // row_shl:4 (lane + 4)
+        const int32_t dn = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4 (lane - 4)
+        return (lane_id() & 4) ? dn : up;
+    } else if constexpr (J == 8) {
+        return __builtin_amdgcn_update_dpp(0, x, 0x128, 0xf, 0xf, false);   // row_ror:8
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)x, (uint32_t)x, false, false);
+        return (int32_t)((int32_t)r[0] == x ? r[1] : r[0]);
+    } else {
+        static_assert(J == 32, "lane_xor: J in {1, 2, 4, 8, 16, 32}");
+        const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)x, (uint32_t)x, false, false);
+        return (int32_t)((int32_t)r[0] == x ? r[1] : r[0]);
+    }
+}
+__device__ __forceinline__ int32_t lane_xor(int32_t x, int j) {   // j a compile-time constant after unrolling
+    switch (j) {
+        case 1: return lane_xor<1>(x);
+        case 2: return lane_xor<2>(x);
+        case 4: return lane_xor<4>(x);
+        case 8: return lane_xor<8>(x);
+        case 16: return lane_xor<16>(x);
+        default: return lane_xor<32>(x);
+    }
+}
+
 // Bitonic sort of buf[0..n), n <= 64*E, in registers: element i = k*64 + lane lives in x[k];
 // exchanges at distance >= 64 stay inside a lane, shorter ones are lane-xor shuffles.
 // Padding is INT32_MAX; one load and one store per element.
@@ -1106,7 +1142,7 @@ __device__ __forceinline__ void reg_bitonic_sort(int32_t *buf, int32_t n) {
 #pragma unroll
                 for (int k = 0; k < E; k++) {
                     const int i = k * WAVE + ln;
-                    const int32_t y = __shfl_xor(x[k], j, WAVE);
+                    const int32_t y = lane_xor(x[k], j);
                     x[k] = (((i & j) == 0) == ((i & kk) == 0)) ? min(x[k], y) : max(x[k], y);
                 }
             }
