@@ -36,7 +36,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.4 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.5 (gfx950, event walk)"
 
 namespace {
 
@@ -570,7 +570,8 @@ __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141:
 #endif
 #ifndef SVT_DIAG
 #define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 2 = no chunk
-                                 // resolve (index walk), 3 = no refine_end stop search (event walk), 4 = no vote
+                                 // resolve (index walk), 3 = no refine_end stop search (event walk), 4 = no sort/vote,
+                                 // 5 = sort + prefix sums, no vote
 #endif
 // LEAN: the mid-tile overflow flush (rare), which must leave the walk's registers alone:
 // one 16-B half of the chunk in flight at a time.
@@ -1118,14 +1119,16 @@ __device__ __forceinline__ int32_t lane_xor(int32_t x, int j) {   // j a compile
 // Bitonic sort of buf[0..n), n <= 64*E, in registers: element i = k*64 + lane lives in x[k];
 // exchanges at distance >= 64 stay inside a lane, shorter ones are lane-xor shuffles.
 // Padding is INT32_MAX; one load and one store per element.
-template <int E>
+// NB < 64 (E == 1, n <= NB): the merge stages stop at block size NB; the padding above NB
+// stays in place (every exchange of a stage with block size kk stays inside its block).
+template <int E, int NB = E * WAVE>
 __device__ __forceinline__ void reg_bitonic_sort(int32_t *buf, int32_t n) {
     const int ln = lane_id();
     int32_t x[E];
 #pragma unroll
     for (int k = 0; k < E; k++) x[k] = k * WAVE + ln < n ? buf[k * WAVE + ln] : INT32_MAX;
 #pragma unroll
-    for (int kk = 2; kk <= E * WAVE; kk <<= 1) {
+    for (int kk = 2; kk <= NB; kk <<= 1) {
 #pragma unroll
         for (int j = kk >> 1; j > 0; j >>= 1) {
             if (j >= WAVE) {
@@ -1299,7 +1302,9 @@ template <int VOTE>
 __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
                                                  int32_t &support) {
     const int ln = lane_id();
-    if (n <= WAVE) reg_bitonic_sort<1>(buf, n);
+    if (n <= 16) reg_bitonic_sort<1, 16>(buf, n);
+    else if (n <= 32) reg_bitonic_sort<1, 32>(buf, n);
+    else if (n <= WAVE) reg_bitonic_sort<1>(buf, n);
     else if (n <= 2 * WAVE) reg_bitonic_sort<2>(buf, n);
     else if (n <= 4 * WAVE) reg_bitonic_sort<4>(buf, n);
     else {
@@ -1319,6 +1324,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
         carry = (int64_t)rdlane64((uint64_t)s, WAVE - 1);
     }
     wave_sync();
+    if (SVT_DIAG == 5) return n;   // diagnostic build: sort + prefix sums, no vote
     if (VOTE == V_SLIDING) return sw_vote(buf, P, n, k, support);
     return vote(buf, P, n, pos, k);
 }
