@@ -151,6 +151,20 @@ def test_empty_inputs(engine_factory):
     assert (got["start"] == SVT_NA).all() and (got["end"] == SVT_NA).all()
 
 
+def test_load_stats(engine_factory):
+    """svt_last_load_stats: the split of svt_load_pileup's time (host pass, H2D, device index)."""
+    from svtrek_amd.pileup import from_reads
+    eng = engine_factory()
+    eng.load_pileup(from_reads(3, []))
+    st = eng.load_stats()
+    assert st["index_ms"] == 0.0 and st["total_ms"] >= st["host_ms"] >= 0.0
+    r = sim.generate(sim.SimConfig(seed=5, n_targets=2, n_loci=32, coverage=10.0))
+    eng.load_pileup(r.pileup)
+    st = eng.load_stats()
+    assert st["index_ms"] > 0.0 and st["upload_ms"] > 0.0
+    assert st["host_ms"] + st["upload_ms"] <= st["total_ms"] + 1e-3
+
+
 @pytest.mark.parametrize("name", ["cfg1_100del_10x"])
 def test_workload_cfg1_full(engine_factory, name):
     r = sim.generate(sim.WORKLOADS[name])
