@@ -15,7 +15,7 @@ run() {  # name, timeout, args...
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
   tail -1 "$OUT/$name.log"
 }
-run cfg2 400 --steps 20 --warmup 3
+[ "${SKIP_CFG2:-0}" = 1 ] || run cfg2 400 --steps 20 --warmup 3
 run cfg4 400 --workload cfg4_1m_delins_30x_hifi --steps 10 --warmup 2 --no-cpu-baseline
-#run cfg3 600 --workload cfg3_50k_delins_30x_ont --steps 10 --warmup 2 --no-cpu-baseline
+run cfg3 600 --workload cfg3_50k_delins_30x_ont --steps 10 --warmup 2 --no-cpu-baseline
 #run cfg5q 900 --workload cfg5_100k_60x_ul_ont --scale 0.25 --steps 10 --warmup 2 --no-cpu-baseline
