@@ -36,7 +36,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.5 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.6 (gfx950, event walk)"
 
 namespace {
 
@@ -911,8 +911,10 @@ __device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0
 // Row-parallel form of break_after for refine_end's soft-clip stops: up to 4 breaking reads
 // at once, one 16-lane row each (DPP row shifts never cross a row).  Lanes of row g take
 // read `l` = the g-th set bit of `m` (block lane), consume those bits, and push after + 1.
-__device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, int64_t rb, uint64_t m, uint32_t ncig_v,
-                                              uint32_t rpos_v, uint32_t e, Sink &sink) {
+// A read's arena offset is its contig's first offset `cbase` plus rec.w's 32-bit difference
+// (a contig's arena spans < 2^31 words, svt_load_pileup), so no off64 load is on this path.
+__device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t cbase, uint64_t m, uint32_t ncig_v,
+                                              uint32_t rpos_v, uint32_t offlo_v, uint32_t e, Sink &sink) {
     const int ln = lane_id(), g = ln >> 4, t = ln & 15;
     int my = -1;
 #pragma unroll
@@ -926,7 +928,8 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, int64_t rb, ui
     // per-row read parameters (a bpermute from the read's block lane)
     const uint32_t ncig = (uint32_t)__shfl((int)ncig_v, has ? my : 0, WAVE);
     const uint32_t rpos = (uint32_t)__shfl((int)rpos_v, has ? my : 0, WAVE);
-    const uint64_t op0 = has ? P.off64[rb + my] : 0ull;
+    const uint32_t offlo = (uint32_t)__shfl((int)offlo_v, has ? my : 0, WAVE);
+    const uint64_t op0 = has ? cbase + (uint64_t)(offlo - (uint32_t)cbase) : 0ull;
     const uint64_t c0 = op0 / CHUNK;
     const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
     bool found = false;
@@ -979,6 +982,8 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
 #endif
     const int ln = lane_id();
     uint32_t live_ops = 0;   // COUNT builds
+    // the contig's first arena offset (stop_rows' reads' offsets from their rec.w)
+    const uint64_t cbase = KIND == K_END ? P.off64[P.tid_off[tid]] : 0ull;
     for (int64_t rb = lo; rb < hi; rb += WAVE) {
         const int64_t r = rb + ln;
         const bool inb = r < hi;
@@ -1028,7 +1033,7 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
             const bool stop = live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
             sink.push(stop && !brk, (int32_t)(wend + 1u));
             uint64_t m = COUNT || SVT_DIAG == 3 ? 0ull : ballot(stop && brk);
-            while (m) m = stop_rows(P, rb, m, ncig, rpos, e, sink);
+            while (m) m = stop_rows(P, cbase, m, ncig, rpos, rc.w, e, sink);
         }
         if (COUNT) {   // ops walked: every op up to the break op, or all ops; + the soft-clip test word
             uint64_t m = ballot(live);
