@@ -36,7 +36,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.6 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.7 (gfx950, event walk)"
 
 namespace {
 
@@ -1127,7 +1127,7 @@ __device__ __forceinline__ int32_t lane_xor(int32_t x, int j) {   // j a compile
 // NB < 64 (E == 1, n <= NB): the merge stages stop at block size NB; the padding above NB
 // stays in place (every exchange of a stage with block size kk stays inside its block).
 template <int E, int NB = E * WAVE>
-__device__ __forceinline__ void reg_bitonic_sort(int32_t *buf, int32_t n) {
+__device__ __forceinline__ int32_t reg_bitonic_sort(int32_t *buf, int32_t n) {   // returns element ln
     const int ln = lane_id();
     int32_t x[E];
 #pragma unroll
@@ -1159,6 +1159,7 @@ __device__ __forceinline__ void reg_bitonic_sort(int32_t *buf, int32_t n) {
     wave_sync();
 #pragma unroll
     for (int k = 0; k < E; k++) buf[k * WAVE + ln] = x[k];
+    return x[0];
 }
 
 __device__ __forceinline__ int32_t ref_abs(int32_t a) { return a < 0 ? -a : a; }   // refinement.h:41
@@ -1307,11 +1308,12 @@ template <int VOTE>
 __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
                                                  int32_t &support) {
     const int ln = lane_id();
-    if (n <= 16) reg_bitonic_sort<1, 16>(buf, n);
-    else if (n <= 32) reg_bitonic_sort<1, 32>(buf, n);
-    else if (n <= WAVE) reg_bitonic_sort<1>(buf, n);
-    else if (n <= 2 * WAVE) reg_bitonic_sort<2>(buf, n);
-    else if (n <= 4 * WAVE) reg_bitonic_sort<4>(buf, n);
+    int32_t x0 = 0;   // sorted element ln, from the register sorts (no LDS read-back below)
+    if (n <= 16) x0 = reg_bitonic_sort<1, 16>(buf, n);
+    else if (n <= 32) x0 = reg_bitonic_sort<1, 32>(buf, n);
+    else if (n <= WAVE) x0 = reg_bitonic_sort<1>(buf, n);
+    else if (n <= 2 * WAVE) x0 = reg_bitonic_sort<2>(buf, n);
+    else if (n <= 4 * WAVE) x0 = reg_bitonic_sort<4>(buf, n);
     else {
         int N = 1;
         while (N < n) N <<= 1;
@@ -1323,7 +1325,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
     if (ln == 0) P[0] = 0;
     for (int32_t b = 0; b < n; b += WAVE) {
         int32_t i = b + ln;
-        int64_t x = i < n ? (int64_t)buf[i] : 0;
+        int64_t x = i < n ? (int64_t)(b == 0 && n <= 4 * WAVE ? x0 : buf[i]) : 0;
         int64_t s = carry + wave_scan_add64(x);
         if (i < n) P[i + 1] = s;
         carry = (int64_t)rdlane64((uint64_t)s, WAVE - 1);
