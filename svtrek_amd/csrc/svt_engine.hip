@@ -36,7 +36,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.7 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.8.8 (gfx950, event walk)"
 
 namespace {
 
@@ -1200,7 +1200,9 @@ __device__ __forceinline__ int32_t mean_cluster(int64_t tot, int32_t cnt, int32_
 }
 
 // consensus_pos (refinement.c:41-101) on sorted A[0..n) with prefix sums P[0..n].
-__device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t pos, const KParams &k) {
+// reg: x0 holds A[lane] for lanes < min(n, 64) (the register sorts), read instead of LDS.
+__device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t pos, const KParams &k,
+                                        int32_t x0, bool reg) {
     const int ln = lane_id();
     const int32_t ci = k.ci, range = k.range;
     int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
@@ -1210,7 +1212,7 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
     int32_t u = 0;
     for (int32_t b = 0; b < n; b += WAVE) {
         int32_t i = b + ln;
-        u += __popcll(ballot(i < n && A[i] <= pos + SV_MIN_LENGTH / 2));
+        u += __popcll(ballot(i < n && (reg && b == 0 ? x0 : A[i]) <= pos + SV_MIN_LENGTH / 2));
     }
     int32_t p = u == 0 ? 0 : u - 1;
 
@@ -1241,15 +1243,16 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
     }
 
     // upper_bound(A, n, pos-25): 0 if A[0] < pos-25 else n-1   (refinement.c:12-19)
-    int32_t q = (n > 0 && A[0] < pos - SV_MIN_LENGTH / 2) ? 0 : n - 1;
+    int32_t q = (n > 0 && (reg ? rdlane_i(x0, 0) : A[0]) < pos - SV_MIN_LENGTH / 2) ? 0 : n - 1;
     for (int32_t bot = q; bot < n; bot += WAVE) {
         int32_t i = bot + ln;
-        bool inr = i < n && ref_abs(pos - A[i < n ? i : 0]) < range;
+        const int32_t ai = reg && bot == 0 ? x0 : A[i < n ? i : 0];
+        bool inr = i < n && ref_abs(pos - ai) < range;
         uint64_t stop = ballot(!inr);
         int lim = stop ? __builtin_ctzll(stop) : WAVE;
         int32_t cnt = 0, cand = 0;
         if (ln < lim) {
-            int32_t a = A[i];
+            int32_t a = ai;
             int32_t m = first_greater(A, i + 1, n, (int64_t)a + ci);   // contiguous j>i with A[j] <= a+ci
             cnt = m - i;
             cand = mean_cluster(P[m] - P[i], cnt, a);
@@ -1333,7 +1336,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
     wave_sync();
     if (SVT_DIAG == 5) return n;   // diagnostic build: sort + prefix sums, no vote
     if (VOTE == V_SLIDING) return sw_vote(buf, P, n, k, support);
-    return vote(buf, P, n, pos, k);
+    return vote(buf, P, n, pos, k, x0, n <= 4 * WAVE);
 }
 
 struct WinLds {
