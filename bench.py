@@ -3,27 +3,32 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-A step = one refinement pass of the HIP engine (svt_refine_device, one batched launch)
-over one rank's shard of SV loci, with the pileup and loci already resident in HBM.
-N>1: every rank owns its own shard (independent loci, no data-path collective: weak
-scaling); each step ends with the one RCCL gather of refined calls to rank 0 that the
-multi-GPU path performs.  Rank 0 prints ONE JSON line.
+Workload: BASELINE config 4 by default (cfg4_1m_delins_30x_hifi: 1M DEL+INS calls over 22
+contigs, 30x HiFi-like pileup) -- the configuration the >= 100k loci/s target is quoted on.
+Every rank generates the same seeded workload; the loci are put in genomic order and rank g
+refines the g-th contiguous slice against only the reads its queries can reach
+(distributed.shard_workload), so the total work is fixed as N grows
+("scaling": "strong").  A step = one batched launch of the HIP engine over the rank's slice
+(svt_refine_device_records: pileup, loci and results resident in HBM) and, at N > 1, the one
+collective of the path: an RCCL gather to rank 0 of the slice's 16-B {vcf_index, start, end,
+pad} records, padded to ceil(N_total / N) rows; the gather of step i overlaps the launch of
+step i + 1 (double-buffered records).  Rank 0 prints ONE JSON line.
 
-roofline: algorithmic bytes of the timed kernel (refine_event_kernel) per launch =
-  16 B/locus in + 8 B/locus out + Σ_windows Σ_yielded reads (12 B + 4 B × CIGAR words walked)
-(what the reference's walk touches; counted exactly by svt_count_work) ÷ the
-kernel's mean duration, measured with HIP events on the launch stream.  The event walk reads
-per-read summaries built once by svt_load_pileup (candidate-op lists, walk ends, chunk index)
-instead of every CIGAR word, so `achieved` can exceed the HBM peak; `traffic` (measured HBM
-bytes per launch, rocprofv3 PMC, profiles/traffic.json) and `traffic_frac` give the kernel's
-physical bandwidth.  cpu_baseline: the CPU oracle (restatement of the reference's tpool path
-over the same in-memory pileup) timed on rank 0's host cores on the same workload.
+roofline (the timed kernel, refine_event_kernel): `achieved` = the event walk's algorithmic
+bytes per launch (svt_work.event_bytes, counted exactly by svt_count_work; DESIGN.md
+"Roofline") / the kernel's mean launch time from HIP events on the launch stream.  `ref_walk`
+keeps SURVEY.md §8(d)'s figure (the bytes the reference's CIGAR walk touches) against index
+build + launch time.  `traffic` = HBM bytes per launch from the committed rocprofv3 PMC passes
+of this engine version and workload (profiles/traffic.json, tools/make_traffic.py).
+cpu_baseline: the CPU oracle (restatement of the reference's tpool path) on rank 0's host cores.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import statistics
 import sys
 import time
 
@@ -31,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+DEFAULT_WORKLOAD = "cfg4_1m_delins_30x_hifi"
 
 
 def _cpu_model() -> str:
@@ -44,13 +50,29 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(res, n_threads: int, budget_s: float = 20.0) -> dict:
+def cpu_cores() -> tuple[int, int, float | None]:
+    """(cores to use, CPUs in this process's affinity mask, cgroup CPU quota or None)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return n, aff, quota
+
+
+def cpu_baseline(res, loci, n_threads: int, budget_s: float = 24.0) -> dict:
     """Time the CPU oracle (reference-shaped restatement, T pthread workers) on a bounded
     sample of the same workload.  Test-infrastructure leg: the only bench use of oracle/."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ffi as O  # noqa: E402
-
-    loci = res.loci
 
     def timed(n: int, threads: int, min_s: float) -> tuple[float, int]:
         """loci/s over repeated passes on loci[:n] until at least min_s of wall time."""
@@ -68,14 +90,24 @@ def cpu_baseline(res, n_threads: int, budget_s: float = 20.0) -> dict:
     per_locus_1t = max(time.perf_counter() - t, 1e-6) / n0
     n1 = int(min(len(loci), max(n0, budget_s / 3 / per_locus_1t)))
     v1, d1 = timed(n1, 1, budget_s / 3)
-    vt, dt_ = timed(len(loci), n_threads, budget_s * 2 / 3)
-    return {
+    nt = int(min(len(loci), max(n0, budget_s * 2 / 3 / per_locus_1t * n_threads / 4)))
+    vt, dt_ = timed(nt, n_threads, budget_s * 2 / 3)
+    out = {
         "value": round(vt, 1), "unit": "loci/s", "cores": n_threads, "kind": "port",
-        "sample": f"all {len(loci)} loci of the same workload, repeated for >= {budget_s * 2 / 3:.0f} s "
-                  f"({dt_} loci), in-memory columnar pileup (no BGZF inflate), {n_threads} pthread workers on "
-                  f"{_cpu_model()}; 1 thread: {v1:.1f} loci/s over {d1} loci (first {n1})",
-        "value_1thread": round(v1, 1),
+        "sample": f"first {nt} loci of the workload (VCF order), repeated for >= {budget_s * 2 / 3:.0f} s "
+                  f"({dt_} loci), {n_threads} pthread workers on {_cpu_model()}; in-memory columnar pileup; "
+                  f"1 thread: {v1:.1f} loci/s over {d1} loci (first {n1})",
+        "value_inmem": round(vt, 1),
+        "value_inmem_1thread": round(v1, 1),
+        "cpu_model": _cpu_model(),
     }
+    try:   # the BGZF leg (per-query BAI lookup + block inflate + record decode, as htslib)
+        from oracle import bgzf_baseline as BB  # noqa: E402
+        out.update(BB.run(res, loci, n_threads, budget_s=budget_s))
+        out["value"] = out.get("value_bgzf", out["value"])
+    except ImportError:
+        pass
+    return out
 
 
 def _engine_version() -> str:
@@ -83,26 +115,42 @@ def _engine_version() -> str:
     return version()
 
 
+def _traffic(workload: str, kernel: str, records: bool) -> tuple[int | None, str | None]:
+    """HBM bytes per launch of this engine version / workload / kernel from the committed
+    rocprofv3 PMC passes (tools/make_traffic.py -> profiles/traffic.json), or (None, None)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for e in tj if isinstance(tj, list) else [tj]:
+        if (e.get("engine_version") == _engine_version() and e.get("workload") == workload
+                and e.get("kernel") == kernel and bool(e.get("records", False)) == records):
+            return int(e["hbm_bytes_per_launch"]), e.get("source")
+    return None, None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="cfg2_10kdel_30x_ont")
+    ap.add_argument("--workload", default=DEFAULT_WORKLOAD)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cold", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--scale", type=float, default=1.0,
                     help="diagnostic: scale the workload's locus count (and so its genome) by this factor")
-    ap.add_argument("--replicate", type=int, default=1,
-                    help="diagnostic: launch the workload's loci R times per step (tail-effect study)")
     args = ap.parse_args()
 
+    import numpy as np
     import torch
     import torch.distributed as dist
 
     from svtrek_amd import Engine, Params, sim
-    from svtrek_amd._lib import RESULT_DTYPE
+    from svtrek_amd._lib import RECORD_DTYPE
+    from svtrek_amd.distributed import PipelinedGather, padded_rows, shard_workload, unpack_records
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -114,54 +162,53 @@ def main() -> int:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
 
-    # ---- synthetic workload (BASELINE config), one shard per rank (weak scaling)
+    # ---- the workload (BASELINE config), identical on every rank; this rank's genomic slice
     cfg = sim.WORKLOADS[args.workload]
     if args.scale != 1.0:
         from dataclasses import replace
         cfg = replace(cfg, n_loci=max(1, int(cfg.n_loci * args.scale)))
-    if world > 1:
-        from dataclasses import replace
-        cfg = replace(cfg, seed=cfg.seed + 1000 * rank)
     t0 = time.perf_counter()
     res = sim.generate(cfg)
     gen_s = time.perf_counter() - t0
-    n = len(res.loci)
-
-    eng = Engine(Params(), device=dev.index)
+    params = Params()
     t0 = time.perf_counter()
-    eng.load_pileup(res.pileup)
+    rows, sl, spile = shard_workload(res.loci, res.pileup, params, world, rank)
+    shard_s = time.perf_counter() - t0
+    n_total, n = len(res.loci), len(sl)
+    per = padded_rows(n_total, world)
+
+    eng = Engine(params, device=dev.index)
+    t0 = time.perf_counter()
+    eng.load_pileup(spile)
     load_s = time.perf_counter() - t0
     load_stats = eng.load_stats()
-    work = eng.count_work(res.loci)   # exact algorithmic work (diagnostic launch, untimed)
+    work = eng.count_work(sl)   # exact algorithmic work (counting kernel, untimed)
 
-    if args.replicate > 1:
-        import numpy as np
-        res.loci = np.tile(res.loci, args.replicate)
-        n = len(res.loci)
-        work = {k: v * args.replicate for k, v in work.items()}
-    loci_np = res.loci.view("u1").reshape(-1)
-    d_loci = torch.from_numpy(loci_np.copy()).to(dev)
-    d_out = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_loci = torch.from_numpy(np.ascontiguousarray(sl).view(np.uint8).copy()).to(dev)
+    d_index = torch.from_numpy(rows.astype(np.uint32).view(np.int32)).to(dev)
+    rec_words = per * RECORD_DTYPE.itemsize // 4
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    gather_list = None
-    if world > 1 and not args.no_gather:
-        gather_list = [torch.empty_like(d_out) for _ in range(world)] if rank == 0 else None
+    gather = world > 1 and not args.no_gather
+    pg = PipelinedGather(lambda: torch.full((rec_words,), -1, dtype=torch.int32, device=dev),   # pads: index ~0
+                         world, rank, enabled=gather)
 
-    def step():
-        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), sh)
-        if world > 1 and not args.no_gather:
-            dist.gather(d_out, gather_list, dst=0)
+    def launch(i: int) -> None:
+        eng.refine_device_records(d_loci.data_ptr(), n, pg.buffer(i).data_ptr(), d_index.data_ptr(), 0, sh)
 
-    for _ in range(args.warmup):
-        step()
+    def step(i: int) -> None:
+        launch(i)
+        pg.submit(i)
+
+    for i in range(args.warmup):
+        step(i)
+    pg.drain()
     eng.sync(sh)
 
-    # HIP events on the launch stream bracket the timed launches: with N = 1 nothing else runs
-    # on that stream, so (end - start) / K is the kernel's average launch duration (plus the
-    # few-us dispatch gap between back-to-back launches; no per-launch event packets in the
-    # timed loop).  N > 1: per-launch event pairs, since the gathers share the stream order.
-    per_launch = world > 1 and not args.no_gather
+    # HIP events on the launch stream: N = 1 -> one pair around the K launches (nothing else
+    # runs on that stream; / K = mean launch duration incl. the dispatch gap); N > 1 -> a pair
+    # per launch (gather waits are interleaved on the stream).
+    per_launch = gather
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps if per_launch else 1)]
     if world > 1:
@@ -172,32 +219,25 @@ def main() -> int:
         ev[0][0].record(stream)
     for i in range(args.steps):
         if per_launch:
+            buf = pg.buffer(i)
             ev[i][0].record(stream)
-        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), sh)
-        if per_launch:
+            eng.refine_device_records(d_loci.data_ptr(), n, buf.data_ptr(), d_index.data_ptr(), 0, sh)
             ev[i][1].record(stream)
-            dist.gather(d_out, gather_list, dst=0)
+            pg.submit(i)
+        else:
+            step(i)
     if not per_launch:
         ev[0][1].record(stream)
+    pg.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     eng.sync(sh)   # raises on a deferred spill-pool overflow
     if per_launch:
-        kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-        kern_mean_ms = sum(kern_ms) / len(kern_ms)
+        kern_mean_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     else:
         kern_mean_ms = ev[0][0].elapsed_time(ev[0][1]) / args.steps
-    # per-launch event pairs in a short untimed pass after the timed region (diagnostic: the
-    # launch-duration spread; includes each pair's own event-packet overhead)
-    pl = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-    for a_, b_ in pl:
-        a_.record(stream)
-        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), sh)
-        b_.record(stream)
-    torch.cuda.synchronize(dev)
-    kern_ms = sorted(a_.elapsed_time(b_) for a_, b_ in pl)
 
     t_max = wall
     if world > 1:
@@ -205,33 +245,54 @@ def main() -> int:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
 
-    total_loci = n * world * args.steps
-    value = total_loci / t_max
-    alg_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
-    achieved = alg_bytes / (kern_mean_ms * 1e-3) / 1e9
+    # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records)
+    last = (args.steps - 1) % 2
+    verified = None
+    if rank == 0 and (gather or world == 1):
+        parts = pg.gathered(last)
+        unpack_records(np.concatenate([p.cpu().numpy().view(np.uint32) for p in parts]), n_total)
+        verified = True
 
-    # HBM traffic of the timed kernel from the committed rocprofv3 PMC passes, when they were
-    # taken on this engine version, workload and kernel (tools/gpu_profile.sh -> profiles/traffic.json)
-    gather = os.environ.get("SVTREK_GATHER", "event")
-    kernel = {"event": "refine_event_kernel", "index": "refine_index_kernel"}.get(gather, "refine_kernel")
-    traffic = traffic_src = None
-    try:
-        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
-            tj = json.load(f)
-        if (tj.get("engine_version") == _engine_version() and tj.get("workload") == args.workload
-                and tj.get("kernel") == kernel and args.replicate == 1):
-            traffic, traffic_src = int(tj["hbm_bytes_per_launch"]), tj.get("source")
-    except (OSError, ValueError, KeyError):
-        pass
+    # ---- untimed: per-launch durations, warm and with the Infinity Cache flushed first
+    pl = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for a_, b_ in pl:
+        a_.record(stream)
+        launch(0)
+        b_.record(stream)
+    torch.cuda.synchronize(dev)
+    warm_ms = sorted(a_.elapsed_time(b_) for a_, b_ in pl)
+    cold_ms = None
+    if not args.no_cold:
+        flush = torch.empty(1 << 30, dtype=torch.uint8, device=dev)   # 4x the 256 MiB MALL
+        cold = []
+        for k in range(3):
+            flush.fill_(k + 1)
+            a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a_.record(stream)
+            launch(0)
+            b_.record(stream)
+            torch.cuda.synchronize(dev)
+            cold.append(a_.elapsed_time(b_))
+        cold_ms = statistics.median(cold)
+        del flush
+
+    total_loci = n_total * args.steps
+    value = total_loci / t_max
+    ev_bytes = int(work["event_bytes"]) + 12 * n   # records: 16-B result record (not 8) + 4-B row index
+    achieved = ev_bytes / (kern_mean_ms * 1e-3) / 1e9
+    ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
+    ref_ms = kern_mean_ms + load_stats["index_ms"]
+    kernel = "refine_event_kernel"
+    traffic, traffic_src = _traffic(args.workload, kernel, records=True)
+    if args.scale != 1.0 or world > 1:
+        traffic = traffic_src = None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            avail = len(os.sched_getaffinity(0))
-        except AttributeError:
-            avail = os.cpu_count() or 1
-        threads = args.cpu_threads or max(1, min(16, avail))
-        cpu = cpu_baseline(res, threads)
+        cores, aff, quota = cpu_cores()
+        cpu = cpu_baseline(res, sl, args.cpu_threads or cores)
+        cpu["affinity_cpus"] = aff
+        cpu["cgroup_cpu_quota"] = quota
 
     if rank == 0:
         out = {
@@ -243,39 +304,42 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (seeded simpileup: ONT-like pileup + SV loci; no real BAM)",
-            "config": {"workload": args.workload, "loci_per_gpu": n, "reads_per_gpu": res.pileup.n_reads,
-                       "cigar_ops_per_gpu": res.pileup.n_ops, "coverage": cfg.coverage,
-                       "read_len_mean": cfg.read_len_mean, "parallelism": f"loci-shard x{world}",
-                       "gather": bool(world > 1 and not args.no_gather),
+            "data": "synthetic (seeded simpileup: HiFi/ONT-like pileup + SV loci; no real BAM)",
+            "config": {"workload": args.workload, "loci_total": n_total, "loci_per_gpu": n,
+                       "reads_per_gpu": spile.n_reads, "cigar_ops_per_gpu": spile.n_ops,
+                       "coverage": cfg.coverage, "read_len_mean": cfg.read_len_mean,
+                       "parallelism": f"genomic row shard x{world}",
+                       "gather": "16-B records, RCCL gather to rank 0, overlapped with the next launch"
+                       if gather else None,
                        **({"loci_scale": args.scale} if args.scale != 1.0 else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_over_alg": round(traffic / ev_bytes, 4) if traffic else None,
                          "traffic_gbs": round(traffic / (kern_mean_ms * 1e-3) / 1e9, 2) if traffic else None,
-                         "traffic_frac": round(traffic / (kern_mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
-                         if traffic else None,
                          "traffic_source": traffic_src,
-                         "kernel": kernel, "gather": gather, "kernel_ms_mean": round(kern_mean_ms, 5),
+                         "kernel": kernel, "kernel_ms_mean": round(kern_mean_ms, 5),
                          "kernel_ms_timing": "per-launch event pairs" if per_launch else
                          "one event pair around the timed launches / K",
-                         "kernel_ms_min": round(kern_ms[0], 5),
-                         "kernel_ms_mean_event_pairs": round(sum(kern_ms) / len(kern_ms), 5),
-                         "alg_bytes_per_launch": alg_bytes,
-                         "note": "achieved = the reference walk's bytes (SURVEY 8(d)) / kernel time; the event walk "
-                                 "reads load-time per-read summaries instead of every CIGAR word, so achieved can "
-                                 "exceed peak; traffic = measured HBM bytes per launch" if gather == "event" else None},
-            # the query-independent device index (built once per pileup by svt_load_pileup, like
-            # the reference's BAI) is outside the timed step; for transparency, the throughput
-            # if every step rebuilt it too: loci / (step time + index-kernel time)
+                         "kernel_ms_warm_min": round(warm_ms[0], 5),
+                         "kernel_ms_cold": round(cold_ms, 5) if cold_ms else None,
+                         "alg_bytes_per_launch": ev_bytes,
+                         "alg_bytes": "event walk: 36 B/locus (16 in, 4 row index, 16 record out) + 32 B/query + 4 B/search entry + 32 B/yielded read "
+                                      "+ 16 B/overlap-failing read in range + 8 B/list offset + 8 B/list entry "
+                                      "+ 36 B/stop search + 4 B/stop chunk word (svt_work)",
+                         "ref_walk": {"bytes": ref_bytes, "ms": round(ref_ms, 5),
+                                      "gbs": round(ref_bytes / (ref_ms * 1e-3) / 1e9, 2),
+                                      "note": "SURVEY 8(d) bytes of the reference's CIGAR walk / (device index "
+                                              "build + launch)"}},
             "index_build": {"index_ms": load_stats["index_ms"], "load_ms": load_stats,
                             "value_if_rebuilt_every_step": round(
-                                n * world / (t_max / args.steps + load_stats["index_ms"] * 1e-3), 1)},
+                                n_total / (t_max / args.steps + load_stats["index_ms"] * 1e-3), 1)},
             "cpu_baseline": cpu,
             "work": work,
-            "setup_s": {"generate": round(gen_s, 2), "load_pileup": round(load_s, 2)},
+            "records_verified": verified,
+            "setup_s": {"generate": round(gen_s, 2), "shard": round(shard_s, 2), "load_pileup": round(load_s, 2)},
             "pileup_device_bytes": eng.device_bytes,
             "engine_version": _engine_version(),
         }

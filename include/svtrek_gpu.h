@@ -22,11 +22,17 @@
  * the six refinement fields of t_arg, params.h:81-87).
  *
  * Conventions: plain C types only, no HIP/torch types; every function returns 0
- * (SVT_OK) or a negative svt_status; no exceptions cross the ABI.  One svt_ctx
- * drives one GPU and is used by one host thread at a time; several GPUs = several
- * contexts (one process per GPU in the multi-GPU driver).  Results use the
- * reference's encoding: a breakpoint the vote could not refine is 0xFFFFFFFF
- * (refinement.c returns -1, stored into uint32 at audit.c:179,194).
+ * (SVT_OK) or a negative svt_status; no exceptions cross the ABI.  A context is used by
+ * one host thread at a time (like the reference's per-worker t_arg, audit.c:269-285);
+ * every entry point selects the context's device itself and restores the calling
+ * thread's current device before returning, so one thread may drive several contexts on
+ * several GPUs.  A context opened with svt_open_multi spreads svt_refine_batch /
+ * svt_count_work / svt_sliding_window_ins over its devices internally (the pileup is
+ * replicated: it is a few GB against 288 GB of HBM per MI355X).  Launches of one context
+ * execute in submission order even when issued on different streams (the context
+ * inserts the stream dependency; the spill pool and the work counters are per context).
+ * Results use the reference's encoding: a breakpoint the vote could not refine is
+ * 0xFFFFFFFF (refinement.c returns -1, stored into uint32 at audit.c:179,194).
  */
 #ifndef SVTREK_GPU_H
 #define SVTREK_GPU_H
@@ -105,7 +111,10 @@ typedef struct svt_pileup_view {
     const uint8_t  *clip;       /* [n_reads] SVT_CLIP_* bits, or NULL: derive from cigar */
 } svt_pileup_view;
 
-/* Work counters of one batch (svt_count_work): what the reference algorithm touches. */
+/* Work counters of one batch (svt_count_work).  The first group is what the reference
+ * algorithm touches (24 B/locus + 12 B/yielded read + 4 B/CIGAR word
+ * walked); the second is what the engine's event walk (refine_event_kernel) must read
+ * for the same batch -- its algorithmic bytes are `event_bytes` (DESIGN.md "Roofline"). */
 typedef struct svt_work {
     uint64_t windows;        /* region queries issued (INV windows excluded)             */
     uint64_t reads;          /* reads yielded by the region queries                      */
@@ -113,12 +122,42 @@ typedef struct svt_work {
                                 plus the soft-clip test word when not already walked      */
     uint64_t candidates;     /* breakpoint candidates pushed                              */
     uint64_t spilled_windows;/* windows whose candidates exceeded SVT_LDS_CANDS          */
+    /* event walk (zero for the A/B gather variants) */
+    uint64_t queries;        /* windows whose query reached the bucket table (32 B each)  */
+    uint64_t probe_entries;  /* pos[]/emax[] entries the two searches need, boundary incl. */
+    uint64_t range_reads;    /* reads in the query ranges [lo,hi): yielded (rec+rec2, 32 B)
+                                plus overlap-failing ones (rec only, 16 B)                */
+    uint64_t list_reads;     /* reads whose candidate-op list is read past the inline entry
+                                (one 8-B list offset each)                                */
+    uint64_t list_entries;   /* list entries read past the inline one (8 B each)          */
+    uint64_t stop_searches;  /* refine_end break searches: 8 CIGAR words + 1 chunk word  */
+    uint64_t stop_chunk_words; /* chunk-index words those searches scan, break chunk incl. */
+    uint64_t event_bytes;    /* algorithmic bytes of the batch's event walk (sum of the above
+                                at their byte sizes + 24 B per locus)                     */
 } svt_work;
+
+/* One refined call as the multi-GPU gather moves it: the record's index
+ * in the VCF, its two results, padding.  index == 0xFFFFFFFF marks gather padding. */
+typedef struct svt_record {
+    uint32_t index;
+    uint32_t start;
+    uint32_t end;
+    uint32_t pad;
+} svt_record;
 
 typedef struct svt_ctx svt_ctx;
 
 /* Open a context on HIP device `device` (-1 = current).  Validates params. */
 svt_status svt_open(const svt_params *params, int device, svt_ctx **out);
+
+/* Open one context over `device_count` GPUs (devices[i], or 0 .. device_count-1 when
+ * devices is NULL).  svt_load_pileup replicates the pileup on every device;
+ * svt_refine_batch / svt_count_work / svt_sliding_window_ins split their batch into
+ * contiguous slices, one per device, run concurrently and return results in input order.
+ * The device-pointer calls (svt_refine_device*, svt_sync) and the POA mode act on the
+ * first device.  device_count == 1 is svt_open(params, devices ? devices[0] : 0, out). */
+svt_status svt_open_multi(const svt_params *params, int device_count, const int *devices, svt_ctx **out);
+int        svt_device_count(const svt_ctx *ctx);
 
 /* Copy the pileup to device HBM (replaces any previous one).  Synchronous. */
 svt_status svt_load_pileup(svt_ctx *ctx, const svt_pileup_view *pileup);
@@ -132,7 +171,16 @@ svt_status svt_refine_batch(svt_ctx *ctx, const svt_locus *loci, size_t n, svt_r
 svt_status svt_refine_device(svt_ctx *ctx, const svt_locus *d_loci, size_t n,
                              svt_result *d_out, void *hip_stream);
 
-/* Wait for `hip_stream` and report a deferred error (SVT_EOVERFLOW) of earlier calls. */
+/* As svt_refine_device, but each result is written as a gather record
+ * {d_index[i] (or index_base + i when d_index is NULL), start, end, 0}. */
+svt_status svt_refine_device_records(svt_ctx *ctx, const svt_locus *d_loci, size_t n,
+                                     const uint32_t *d_index, uint32_t index_base,
+                                     svt_record *d_rec, void *hip_stream);
+
+/* Wait for `hip_stream` and report a deferred error (SVT_EOVERFLOW) of earlier calls.
+ * On SVT_EOVERFLOW the context's spill pool has already been grown to what the failed
+ * launch needed: re-running the same batch succeeds.  (svt_refine_batch and
+ * svt_count_work do that re-run themselves.) */
 svt_status svt_sync(svt_ctx *ctx, void *hip_stream);
 
 /* Count the reference algorithm's work for n host loci (diagnostic, synchronous). */

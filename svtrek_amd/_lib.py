@@ -28,6 +28,7 @@ LOCUS_DTYPE = np.dtype([("type", "<i4"), ("chrom", "<i4"), ("pos", "<u4"), ("end
 RESULT_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4")])
 SW_QUERY_DTYPE = np.dtype([("chrom", "<i4"), ("start", "<u4"), ("end", "<u4")])     # svt_sw_query
 SW_WINDOW_DTYPE = np.dtype([("candidate", "<i4"), ("support", "<i4")])               # svt_sw_window
+RECORD_DTYPE = np.dtype([("index", "<u4"), ("start", "<u4"), ("end", "<u4"), ("pad", "<u4")])   # svt_record
 
 
 class SvtParams(C.Structure):
@@ -73,6 +74,14 @@ class SvtWork(C.Structure):
         ("ops_walked", C.c_uint64),
         ("candidates", C.c_uint64),
         ("spilled_windows", C.c_uint64),
+        ("queries", C.c_uint64),
+        ("probe_entries", C.c_uint64),
+        ("range_reads", C.c_uint64),
+        ("list_reads", C.c_uint64),
+        ("list_entries", C.c_uint64),
+        ("stop_searches", C.c_uint64),
+        ("stop_chunk_words", C.c_uint64),
+        ("event_bytes", C.c_uint64),
     ]
 
 
@@ -91,7 +100,8 @@ ENGINE_SYMBOLS = (
     "svt_count_work", "svt_pileup_device_bytes", "svt_last_error", "svt_close", "svt_version",
     "svt_sw_subwindows", "svt_sliding_window_ins",
     "svt_poa_default_params", "svt_pileup_ins_count", "svt_load_insseq", "svt_poa_consensus",
-    "svt_poa_deferred", "svt_last_load_stats",
+    "svt_poa_deferred", "svt_last_load_stats", "svt_open_multi", "svt_device_count",
+    "svt_refine_device_records",
 )
 
 _engine = None
@@ -113,6 +123,10 @@ def load_engine() -> C.CDLL:
     lib = C.CDLL(path)
     P = C.c_void_p
     lib.svt_open.argtypes = [C.POINTER(SvtParams), C.c_int, C.POINTER(P)]
+    lib.svt_open_multi.argtypes = [C.POINTER(SvtParams), C.c_int, P, C.POINTER(P)]
+    lib.svt_device_count.argtypes = [P]
+    lib.svt_device_count.restype = C.c_int
+    lib.svt_refine_device_records.argtypes = [P, P, C.c_size_t, P, C.c_uint32, P, P]
     lib.svt_load_pileup.argtypes = [P, C.POINTER(SvtPileupView)]
     lib.svt_refine_batch.argtypes = [P, P, C.c_size_t, P]
     lib.svt_refine_device.argtypes = [P, P, C.c_size_t, P, P]
@@ -137,7 +151,7 @@ def load_engine() -> C.CDLL:
     lib.svt_poa_consensus.argtypes = [P, C.POINTER(SvtPoaParams), P, P, C.c_size_t, C.c_int32, P, P]
     lib.svt_poa_deferred.argtypes = [P]
     lib.svt_poa_deferred.restype = C.c_uint64
-    for name in ("svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
+    for name in ("svt_open", "svt_open_multi", "svt_refine_device_records", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
                  "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):
         getattr(lib, name).restype = C.c_int32
     _engine = lib

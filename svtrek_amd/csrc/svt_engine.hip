@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <chrono>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/svtrek_gpu.h"
@@ -98,7 +99,16 @@ struct KArgs {
     unsigned long long *work;   // svt_work counters (COUNT builds only)
     const uint4 *sw_sub;        // sliding_window_ins mode: per sub-window {chrom, start, end, 0}
     int2 *sw_out;               //   per sub-window {bestCandidate, maxSupport}
+    uint4 *rec_out;             // gather records {index, start, end, 0} instead of `out` (or null)
+    const uint32_t *rec_index;  //   index of locus i: rec_index[i], or rec_base + i when null
+    uint32_t rec_base;
 };
+
+// svt_work counter slots (refine_window's wk[], the context's work words)
+constexpr int W_WINDOWS = 0, W_READS = 1, W_OPS = 2, W_CANDS = 3, W_SPILLED = 4, W_QUERIES = 5, W_PROBE = 6,
+              W_RANGE = 7, W_LREADS = 8, W_LENTRIES = 9, W_STOPS = 10, W_STOPCH = 11, W_N = 12;
+constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status, work counters
+static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
 
 // ------------------------------------------------------------------ wave primitives
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
@@ -215,6 +225,8 @@ struct Sink {
 
 struct WinStats {
     unsigned long long reads = 0, ops = 0;
+    // event walk's own reads (G_EVENT COUNT builds): see svt_work
+    unsigned long long queries = 0, probe = 0, range = 0, lreads = 0, lentries = 0, stops = 0, stopch = 0;
 };
 
 template <int KIND>
@@ -285,7 +297,7 @@ __device__ __forceinline__ int64_t probe_first(int64_t l, int64_t h, bool hit_in
 }
 
 __device__ __forceinline__ bool read_range(const DevPileup &P, int tid, int64_t beg, int64_t end, int64_t &lo,
-                                           int64_t &hi) {
+                                           int64_t &hi, WinStats *st = nullptr) {
     if (tid < 0 || tid >= P.n_targets || end <= beg) return false;   // no reads (A3)
     const int64_t ra = P.tid_off[tid], nr = P.tid_off[tid + 1] - ra;
     if (nr == 0) return false;
@@ -301,6 +313,10 @@ __device__ __forceinline__ bool read_range(const DevPileup &P, int tid, int64_t 
     int64_t l = probe_first(ll, lh, (int64_t)ev > beg, vl);
     if (hh - hl > WAVE) h = wave_partition_point(hl, hh, [&](int64_t r) { return (int64_t)pos[r] >= end; });
     if (lh - ll > WAVE) l = wave_partition_point(ll, lh, [&](int64_t r) { return (int64_t)emax[r] > beg; });
+    if (st) {   // COUNT builds: the bucket words + each search's entries up to its boundary
+        st->queries++;
+        st->probe += (unsigned long long)((h - hl) + (h < hh ? 1 : 0) + (l - ll) + (l < lh ? 1 : 0));
+    }
     lo = ra + l;
     hi = ra + h;
     return lo < hi;
@@ -976,7 +992,7 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
     if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi)) return;
+    if (!read_range(P, tid, beg, end, lo, hi, COUNT ? &st : nullptr)) return;
 #if SVT_DIAG == 1
     if (lo < hi) return;     // diagnostic build: region query only
 #endif
@@ -1004,10 +1020,12 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
         if (COUNT) {
             st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
             if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
+            st.range += (unsigned long long)__popcll(ballot(inb));
         }
         // candidate ops processed before the break (refinement.c:124-136 / :190-200 / :299-310)
         {
             uint32_t n = live ? r2.y : 0u;
+            const uint32_t n_list = n;
             // the first one is inline in rec2 (most reads carry at most one)
             auto take = [&](uint2 a, uint32_t k) {
                 if (a.x > e) n = k;
@@ -1024,6 +1042,14 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
                     a = k + 2 < n ? evp[k + 2] : make_uint2(0, 0);
                     b = k + 3 < n ? evp[k + 3] : make_uint2(0, 0);
                 }
+            }
+            if (COUNT) {   // entries needed past the inline one: up to the first past inter.end
+                const uint32_t need = n_list ? min(n, n_list - 1u) : 0u;
+                st.lreads += (unsigned long long)__popcll(ballot(need > 0));
+                uint32_t tot = need;
+#pragma unroll
+                for (int d = 32; d > 0; d >>= 1) tot += (uint32_t)__shfl_xor((int)tot, d, WAVE);
+                st.lentries += tot;
             }
         }
         // soft-clip candidates at the walk's stop
@@ -1047,8 +1073,11 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
                     uint32_t bi;
                     const uint32_t aft = break_after(P, P.off64[rb + l], nc, rp, e, bi);
                     walked = bi + 1;
-                    if (KIND == K_END && (rdlane(clip, l) & SVT_CLIP_FIRST_S) && s <= rp && rp <= e && ln == 0)
-                        sink.push1((int32_t)(aft + 1u));
+                    if (KIND == K_END && (rdlane(clip, l) & SVT_CLIP_FIRST_S) && s <= rp && rp <= e) {
+                        if (ln == 0) sink.push1((int32_t)(aft + 1u));
+                        st.stops++;                                   // stop_rows' search for this read:
+                        st.stopch += (unsigned long long)(bi / CHUNK + 1u);   // chunk words to the break chunk
+                    }
                     if (KIND == K_START && bi + 1 != nc) walked++;   // cigar[n-1] test word
                 }
                 if (ln == 0) live_ops += walked;
@@ -1371,14 +1400,16 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     Sink sink{lds.cand, CAP, &lds.ncand};
     int32_t n = gather<KIND, COUNT, G>(a, chrom - 1, s, e, sink, st, lds);
     if (COUNT && lane_id() == 0) {
-        wk[0] += 1; wk[1] += st.reads; wk[2] += st.ops; wk[3] += (unsigned long long)n;
+        wk[W_WINDOWS] += 1; wk[W_READS] += st.reads; wk[W_OPS] += st.ops; wk[W_CANDS] += (unsigned long long)n;
+        wk[W_QUERIES] += st.queries; wk[W_PROBE] += st.probe; wk[W_RANGE] += st.range; wk[W_LREADS] += st.lreads;
+        wk[W_LENTRIES] += st.lentries; wk[W_STOPS] += st.stops; wk[W_STOPCH] += st.stopch;
     }
     support = 0;
     if (n < a.prm.min_count) return -1;                    // refinement.c:43-45 (sliding: no support >= min_count)
     if (SVT_DIAG == 4) return n;   // diagnostic build: no sort/vote
     if (n <= CAP) return sort_and_vote<VOTE>(lds.cand, lds.pre, n, (int32_t)imprecise, a.prm, support);
     // spill: a slab for N ints + (n+1) int64 from the device pool, then re-gather into it
-    if (COUNT && lane_id() == 0) wk[4] += 1;
+    if (COUNT && lane_id() == 0) wk[W_SPILLED] += 1;
     int N = 1;
     while (N < n) N <<= 1;
     unsigned long long words = (unsigned long long)N + 2ull * (unsigned long long)(n + 2);
@@ -1468,7 +1499,7 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
     const svt_locus L = a.loci[li];
     const int32_t type = uniform_i(L.type), chrom = uniform_i(L.chrom);
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
-    unsigned long long wk[5] = {0, 0, 0, 0, 0};
+    unsigned long long wk[W_N] = {};
     uint32_t r = SVT_NA;
     int32_t sup;
     const KParams &k = a.prm;
@@ -1489,10 +1520,19 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
     // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250), so both
     // windows vote on 0 candidates -> -1 for every min_count >= 1 (validated): NA, NA.
     if (lane_id() == 0) {
-        uint32_t *o = reinterpret_cast<uint32_t *>(a.out + li);
-        o[w] = r;
+        if (a.rec_out) {   // gather record {index, start, end, 0}
+            uint32_t *o = reinterpret_cast<uint32_t *>(a.rec_out + li);
+            o[1 + w] = r;
+            if (w == 0) {
+                o[0] = a.rec_index ? a.rec_index[li] : a.rec_base + li;
+                o[3] = 0u;
+            }
+        } else {
+            uint32_t *o = reinterpret_cast<uint32_t *>(a.out + li);
+            o[w] = r;
+        }
         if (COUNT)
-            for (int i = 0; i < 5; i++)
+            for (int i = 0; i < W_N; i++)
                 if (wk[i]) atomicAdd(a.work + i, wk[i]);
     }
 }
@@ -1510,7 +1550,7 @@ __global__ __launch_bounds__(64 * WPB) void sw_kernel(KArgs a) {
     const uint4 q = a.sw_sub[g];
     const int32_t chrom = uniform_i((int32_t)q.x);
     const uint32_t s = (uint32_t)uniform_i((int32_t)q.y), e = (uint32_t)uniform_i((int32_t)q.z);
-    unsigned long long wk[5];
+    unsigned long long wk[W_N];
     int32_t sup = 0;
     const int32_t c = refine_window<K_INS, false, G, V_SLIDING>(a, lds_all[wid], chrom, s, e, 0u, wk, sup);
     if (lane_id() == 0) a.sw_out[g] = make_int2(c, sup);
@@ -1676,8 +1716,14 @@ struct svt_ctx {
     // spill pool + status + work counters
     int32_t *d_pool = nullptr;
     unsigned long long pool_words = 0;
-    unsigned char *d_ctl = nullptr;   // [0,8) pool head (epoch-tagged), [8,12) sticky status, [16,56) work
+    unsigned char *d_ctl = nullptr;   // [0,8) pool head (epoch-tagged), [8,12) sticky status, [16,16+8*W_N) work
     uint32_t epoch = 0;               // launches so far (pool epochs cycle through 1 .. 2^24-1)
+    // launches run in submission order across streams (order_on)
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
+    hipEvent_t order_ev = nullptr;
+    // svt_open_multi: the contexts of devices[1..] (this one drives devices[0])
+    std::vector<svt_ctx *> subs;
 };
 
 namespace {
@@ -1697,6 +1743,56 @@ template <typename T>
 void hfree(T *&p) {
     if (p) (void)hipFree((void *)p);
     p = nullptr;
+}
+
+// Every entry point runs on its context's device and gives the calling thread its current
+// device back (one host thread may drive contexts on several GPUs).
+struct DevGuard {
+    int prev = -1, dev;
+    bool ok = true;
+    explicit DevGuard(int d) : dev(d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DevGuard() {
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+};
+#define DEV_GUARD(ctx)                                                                    \
+    DevGuard dg_((ctx)->device);                                                          \
+    if (!dg_.ok) return fail((ctx), SVT_EDEVICE, "hipSetDevice(%s) failed", "ctx device")
+
+// A context's launches share its spill pool (epoch-tagged head), sticky status and work
+// counters, so they must not overlap: a launch on another stream than the previous one
+// first waits for everything issued so far on that one.
+svt_status order_on(svt_ctx *c, hipStream_t st) {
+    if (c->have_last && st != c->last_stream) {
+        if (!c->order_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+        HIP_TRY(c, hipEventRecord(c->order_ev, c->last_stream));
+        HIP_TRY(c, hipStreamWaitEvent(st, c->order_ev, 0));
+    }
+    c->last_stream = st;
+    c->have_last = true;
+    return SVT_OK;
+}
+
+// After a launch reported the spill pool exhausted: the head word of that launch's epoch
+// holds every word its spilled windows asked for (svt_refine_*'s CAS adds them even past
+// the end); grow the pool to that, at least doubling it.
+svt_status grow_pool(svt_ctx *c) {
+    unsigned long long head = 0;
+    HIP_TRY(c, hipDeviceSynchronize());
+    HIP_TRY(c, hipMemcpy(&head, c->d_ctl, 8, hipMemcpyDeviceToHost));
+    const uint64_t need = (uint32_t)(head >> 40) == c->epoch ? (head & ((1ull << 40) - 1ull)) : 0ull;
+    const uint64_t words = std::max<uint64_t>(need + need / 8 + 1024, 2 * c->pool_words);
+    hfree(c->d_pool);
+    c->pool_words = 0;
+    if (hipMalloc(&c->d_pool, words * 4) != hipSuccess) {
+        c->d_pool = nullptr;
+        return fail(c, SVT_ENOMEM, "%s", "growing the candidate spill pool failed");
+    }
+    c->pool_words = words;
+    return SVT_OK;
 }
 
 void free_pileup(svt_ctx *c) {
@@ -1725,18 +1821,28 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
     a.work = count ? (unsigned long long *)(c->d_ctl + 16) : nullptr;
     a.sw_sub = nullptr;
     a.sw_out = nullptr;
+    a.rec_out = nullptr;
+    a.rec_index = nullptr;
+    a.rec_base = 0;
     return a;
 }
 
-svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t n, hipStream_t st, bool count) {
+svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t n, hipStream_t st, bool count,
+                  svt_record *rec_out = nullptr, const uint32_t *rec_index = nullptr, uint32_t rec_base = 0) {
     if (n == 0) return SVT_OK;
     if (n > 0x3fffffffull) return fail(c, SVT_EINVAL, "batch too large (%s)", "n > 2^30-1");
-    // no per-launch reset of the spill pool (epoch-tagged head); the work counters of a
-    // counting launch start from zero; the head word is cleared once per epoch cycle
+    svt_status s = order_on(c, st);
+    if (s) return s;
+    // no per-launch reset of the spill pool (epoch-tagged head; launches never overlap,
+    // order_on); the work counters of a counting launch start from zero; the head word is
+    // cleared once per epoch cycle
     c->epoch = c->epoch % ((1u << 24) - 1u) + 1u;
     if (c->epoch == 1) HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 8, st));
-    if (count) HIP_TRY(c, hipMemsetAsync(c->d_ctl + 16, 0, 48, st));
+    if (count) HIP_TRY(c, hipMemsetAsync(c->d_ctl + 16, 0, 8 * W_N, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
+    a.rec_out = reinterpret_cast<uint4 *>(rec_out);
+    a.rec_index = rec_index;
+    a.rec_base = rec_base;
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
     if (c->gather == G_EVENT) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_EVENT>), grid, block, 0, st, a);
@@ -1944,19 +2050,21 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
         return SVT_EDEVICE;
     }
     if (device >= 0) {
-        if (device >= ndev || hipSetDevice(device) != hipSuccess) { delete c; return SVT_EDEVICE; }
+        if (device >= ndev) { delete c; return SVT_EDEVICE; }
         c->device = device;
     } else {
         (void)hipGetDevice(&c->device);
     }
+    DevGuard dg(c->device);
+    if (!dg.ok) { delete c; return SVT_EDEVICE; }
     uint64_t pool_bytes = params->spill_bytes ? params->spill_bytes : (64ull << 20);
     c->pool_words = pool_bytes / 4;
-    if (hipMalloc(&c->d_pool, c->pool_words * 4) != hipSuccess || hipMalloc(&c->d_ctl, 64) != hipSuccess) {
+    if (hipMalloc(&c->d_pool, c->pool_words * 4) != hipSuccess || hipMalloc(&c->d_ctl, CTL_BYTES) != hipSuccess) {
         hfree(c->d_pool);
         delete c;
         return SVT_ENOMEM;
     }
-    (void)hipMemset(c->d_ctl, 0, 64);
+    (void)hipMemset(c->d_ctl, 0, CTL_BYTES);
     // load the code object now (HIP loads it lazily at the first launch), so that no later
     // call -- and no timing of one -- pays for it
     hipFuncAttributes fa;
@@ -1965,11 +2073,32 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     return SVT_OK;
 }
 
-svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
+svt_status svt_open_multi(const svt_params *params, int device_count, const int *devices, svt_ctx **out) {
+    if (!params || !out || device_count < 1) return SVT_EINVAL;
+    *out = nullptr;
+    svt_ctx *c = nullptr;
+    svt_status s = svt_open(params, devices ? devices[0] : 0, &c);
+    if (s) return s;
+    for (int i = 1; i < device_count; i++) {
+        svt_ctx *d = nullptr;   // (a device may repeat: two independent contexts on one GPU)
+        s = svt_open(params, devices ? devices[i] : i, &d);
+        if (s) {
+            svt_close(c);
+            return s;
+        }
+        c->subs.push_back(d);
+    }
+    *out = c;
+    return SVT_OK;
+}
+
+int svt_device_count(const svt_ctx *c) { return c ? 1 + (int)c->subs.size() : 0; }
+
+static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if (!c || !p) return SVT_EINVAL;
     if (p->n_targets < 0 || (p->n_targets > 0 && !p->tid_off))
         return fail(c, SVT_EINVAL, "pileup: %s", "bad n_targets / tid_off");
-    HIP_TRY(c, hipSetDevice(c->device));
+    DEV_GUARD(c);
     free_pileup(c);
     using clk = std::chrono::steady_clock;
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
@@ -2128,27 +2257,110 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     return SVT_OK;
 }
 
+// svt_open_multi: run fn(ctx_d, lo_d, hi_d) for the contiguous slices [lo_d, hi_d) of n items,
+// one per device, concurrently (one host thread per extra device); the first failure's
+// status and message are reported on the parent context.
+extern "C++" template <typename F>
+static svt_status for_devices(svt_ctx *c, size_t n, F fn) {
+    const size_t D = 1 + c->subs.size();
+    if (D == 1) return fn(c, (size_t)0, n);
+    std::vector<svt_ctx *> ctx(D);
+    ctx[0] = c;
+    for (size_t d = 1; d < D; d++) ctx[d] = c->subs[d - 1];
+    std::vector<svt_status> st(D, SVT_OK);
+    const size_t per = (n + D - 1) / D;
+    std::vector<std::thread> th;
+    for (size_t d = 1; d < D; d++)
+        th.emplace_back([&, d] { st[d] = fn(ctx[d], std::min(n, d * per), std::min(n, (d + 1) * per)); });
+    st[0] = fn(c, 0, std::min(n, per));
+    for (auto &t : th) t.join();
+    for (size_t d = 0; d < D; d++)
+        if (st[d] != SVT_OK) {
+            if (d) snprintf(c->err, sizeof c->err, "device %d: %s", ctx[d]->device, ctx[d]->err);
+            return st[d];
+        }
+    return SVT_OK;
+}
+
+svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
+    if (!c || !p) return SVT_EINVAL;
+    if (c->subs.empty()) return load_1(c, p);
+    // every device gets the whole pileup (n = device count: one "item" per device)
+    const size_t D = 1 + c->subs.size();
+    return for_devices(c, D, [&](svt_ctx *x, size_t lo, size_t hi) { return lo < hi ? load_1(x, p) : SVT_OK; });
+}
+
 svt_status svt_last_load_stats(const svt_ctx *c, svt_load_stats *out) {
     if (!c || !out) return SVT_EINVAL;
     *out = c->load_stats;
     return SVT_OK;
 }
 
-svt_status svt_refine_device(svt_ctx *c, const svt_locus *d_loci, size_t n, svt_result *d_out, void *stream) {
+static svt_status refine_device_any(svt_ctx *c, const svt_locus *d_loci, size_t n, svt_result *d_out,
+                                    svt_record *d_rec, const uint32_t *d_index, uint32_t index_base, void *stream) {
     if (!c) return SVT_EINVAL;
     if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
-    if (n && (!d_loci || !d_out)) return fail(c, SVT_EINVAL, "%s", "null loci/out");
-    return launch(c, d_loci, d_out, n, (hipStream_t)stream, false);
+    if (n && (!d_loci || (!d_out && !d_rec))) return fail(c, SVT_EINVAL, "%s", "null loci/out");
+    DEV_GUARD(c);
+    return launch(c, d_loci, d_out, n, (hipStream_t)stream, false, d_rec, d_index, index_base);
+}
+
+svt_status svt_refine_device(svt_ctx *c, const svt_locus *d_loci, size_t n, svt_result *d_out, void *stream) {
+    return refine_device_any(c, d_loci, n, d_out, nullptr, nullptr, 0, stream);
+}
+
+svt_status svt_refine_device_records(svt_ctx *c, const svt_locus *d_loci, size_t n, const uint32_t *d_index,
+                                     uint32_t index_base, svt_record *d_rec, void *stream) {
+    if (c && n && !d_rec) return fail(c, SVT_EINVAL, "%s", "null records");
+    return refine_device_any(c, d_loci, n, nullptr, d_rec, d_index, index_base, stream);
 }
 
 svt_status svt_sync(svt_ctx *c, void *stream) {
     if (!c) return SVT_EINVAL;
+    DEV_GUARD(c);
     HIP_TRY(c, hipStreamSynchronize((hipStream_t)stream));
+    if (c->have_last && c->last_stream != (hipStream_t)stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
     int32_t status = 0;
     HIP_TRY(c, hipMemcpy(&status, c->d_ctl + 8, 4, hipMemcpyDeviceToHost));
     if (status & 1) {
         HIP_TRY(c, hipMemset(c->d_ctl + 8, 0, 4));   // sticky until reported
-        return fail(c, SVT_EOVERFLOW, "%s", "candidate spill pool exhausted (raise spill_bytes)");
+        const svt_status g = grow_pool(c);            // a re-run of the batch now fits
+        if (g) return g;
+        return fail(c, SVT_EOVERFLOW, "%s", "candidate spill pool exhausted (pool grown; re-run the batch)");
+    }
+    return SVT_OK;
+}
+
+// One synchronous launch over host loci on one device (count: the work-counting kernel);
+// a launch whose spilled windows outgrew the pool is re-run once the pool has grown.
+static svt_status run_batch_1(svt_ctx *c, const svt_locus *loci, size_t n, svt_result *out, svt_work *w) {
+    if (n == 0) return SVT_OK;
+    DEV_GUARD(c);
+    svt_status s = ensure_batch(c, n);
+    if (s) return s;
+    HIP_TRY(c, hipMemcpy(c->d_loci, loci, n * sizeof(svt_locus), hipMemcpyHostToDevice));
+    for (int attempt = 0;; attempt++) {
+        s = launch(c, c->d_loci, c->d_out, n, nullptr, w != nullptr);
+        if (s) return s;
+        s = svt_sync(c, nullptr);
+        if (s != SVT_EOVERFLOW || attempt == 3) break;
+    }
+    if (s) return s;
+    if (out) HIP_TRY(c, hipMemcpy(out, c->d_out, n * sizeof(svt_result), hipMemcpyDeviceToHost));
+    if (w) {
+        unsigned long long k[W_N];
+        HIP_TRY(c, hipMemcpy(k, c->d_ctl + 16, sizeof k, hipMemcpyDeviceToHost));
+        w->windows = k[W_WINDOWS]; w->reads = k[W_READS]; w->ops_walked = k[W_OPS]; w->candidates = k[W_CANDS];
+        w->spilled_windows = k[W_SPILLED]; w->queries = k[W_QUERIES]; w->probe_entries = k[W_PROBE];
+        w->range_reads = k[W_RANGE]; w->list_reads = k[W_LREADS]; w->list_entries = k[W_LENTRIES];
+        w->stop_searches = k[W_STOPS]; w->stop_chunk_words = k[W_STOPCH];
+        // the event walk's algorithmic bytes (DESIGN.md "Roofline"): locus in + result out,
+        // two bucket words per search, the search entries, rec + rec2 of every yielded read and
+        // rec of every overlap-failing one in range, list offsets and entries, and per stop
+        // search the chunk words scanned, the word before the break chunk and its 8 CIGAR words
+        w->event_bytes = 24ull * n + 32ull * w->queries + 4ull * w->probe_entries + 32ull * w->reads +
+                         16ull * (w->range_reads - std::min(w->range_reads, w->reads)) + 8ull * w->list_reads +
+                         8ull * w->list_entries + 36ull * w->stop_searches + 4ull * w->stop_chunk_words;
     }
     return SVT_OK;
 }
@@ -2158,16 +2370,9 @@ svt_status svt_refine_batch(svt_ctx *c, const svt_locus *loci, size_t n, svt_res
     if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
     if (n == 0) return SVT_OK;
     if (!loci || !out) return fail(c, SVT_EINVAL, "%s", "null loci/out");
-    HIP_TRY(c, hipSetDevice(c->device));
-    svt_status s = ensure_batch(c, n);
-    if (s) return s;
-    HIP_TRY(c, hipMemcpy(c->d_loci, loci, n * sizeof(svt_locus), hipMemcpyHostToDevice));
-    s = launch(c, c->d_loci, c->d_out, n, nullptr, false);
-    if (s) return s;
-    s = svt_sync(c, nullptr);
-    if (s) return s;
-    HIP_TRY(c, hipMemcpy(out, c->d_out, n * sizeof(svt_result), hipMemcpyDeviceToHost));
-    return SVT_OK;
+    return for_devices(c, n, [&](svt_ctx *x, size_t lo, size_t hi) {
+        return run_batch_1(x, loci + lo, hi - lo, out + lo, nullptr);
+    });
 }
 
 svt_status svt_count_work(svt_ctx *c, const svt_locus *loci, size_t n, svt_work *out) {
@@ -2175,18 +2380,20 @@ svt_status svt_count_work(svt_ctx *c, const svt_locus *loci, size_t n, svt_work 
     if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
     memset(out, 0, sizeof(*out));
     if (n == 0) return SVT_OK;
-    HIP_TRY(c, hipSetDevice(c->device));
-    svt_status s = ensure_batch(c, n);
+    if (!loci) return fail(c, SVT_EINVAL, "%s", "null loci");
+    std::vector<svt_work> part(1 + c->subs.size());
+    std::vector<svt_ctx *> who(part.size(), nullptr);
+    const svt_status s = for_devices(c, n, [&](svt_ctx *x, size_t lo, size_t hi) {
+        const size_t d = x == c ? 0 : (size_t)(std::find(c->subs.begin(), c->subs.end(), x) - c->subs.begin()) + 1;
+        memset(&part[d], 0, sizeof(svt_work));
+        return run_batch_1(x, loci + lo, hi - lo, nullptr, &part[d]);
+    });
     if (s) return s;
-    HIP_TRY(c, hipMemcpy(c->d_loci, loci, n * sizeof(svt_locus), hipMemcpyHostToDevice));
-    s = launch(c, c->d_loci, c->d_out, n, nullptr, true);
-    if (s) return s;
-    s = svt_sync(c, nullptr);
-    if (s) return s;
-    unsigned long long w[5];
-    HIP_TRY(c, hipMemcpy(w, c->d_ctl + 16, sizeof w, hipMemcpyDeviceToHost));
-    out->windows = w[0]; out->reads = w[1]; out->ops_walked = w[2]; out->candidates = w[3];
-    out->spilled_windows = w[4];
+    uint64_t *o = reinterpret_cast<uint64_t *>(out);
+    for (const svt_work &p : part) {
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(&p);
+        for (size_t i = 0; i < sizeof(svt_work) / 8; i++) o[i] += q[i];
+    }
     return SVT_OK;
 }
 
@@ -2194,6 +2401,9 @@ uint64_t svt_sw_subwindows(const svt_sw_query *q, int32_t window_size) {
     if (!q || window_size < 1 || q->end <= q->start) return 0;
     return ((uint64_t)(q->end - q->start) + (uint64_t)window_size - 1) / (uint64_t)window_size;
 }
+
+static svt_status sw_1(svt_ctx *c, const svt_sw_query *q, size_t n, int32_t window_size, int32_t slide_size,
+                       int32_t *best, svt_sw_window *sub);
 
 svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, int32_t window_size,
                                   int32_t slide_size, int32_t *best, svt_sw_window *sub) {
@@ -2203,6 +2413,17 @@ svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, i
         return fail(c, SVT_EINVAL, "%s", "window_size and slide_size must be >= 1 (the reference loops forever)");
     if (n == 0) return SVT_OK;
     if (!q || !best) return fail(c, SVT_EINVAL, "%s", "null queries/best");
+    std::vector<uint64_t> soff(n + 1, 0);   // each query's first sub-window in `sub`
+    for (size_t i = 0; i < n; i++) soff[i + 1] = soff[i] + svt_sw_subwindows(q + i, window_size);
+    return for_devices(c, n, [&](svt_ctx *x, size_t lo, size_t hi) {
+        return sw_1(x, q + lo, hi - lo, window_size, slide_size, best + lo, sub ? sub + soff[lo] : nullptr);
+    });
+}
+
+static svt_status sw_1(svt_ctx *c, const svt_sw_query *q, size_t n, int32_t window_size, int32_t slide_size,
+                       int32_t *best, svt_sw_window *sub) {
+    if (n == 0) return SVT_OK;
+    if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
     std::vector<uint64_t> off(n + 1, 0);
     for (size_t i = 0; i < n; i++) {
         if ((uint64_t)q[i].end + (uint64_t)window_size > 0x100000000ull)
@@ -2219,7 +2440,9 @@ svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, i
             subs[(size_t)k] = make_uint4((uint32_t)q[i].chrom, ss, se > q[i].end ? q[i].end : se, 0u);
         }
     }
-    HIP_TRY(c, hipSetDevice(c->device));
+    DEV_GUARD(c);
+    svt_status so = order_on(c, nullptr);
+    if (so) return so;
     uint4 *d_sub = nullptr;
     int2 *d_res = nullptr;
     uint64_t *d_off = nullptr;
@@ -2236,7 +2459,7 @@ svt_status svt_sliding_window_ins(svt_ctx *c, const svt_sw_query *q, size_t n, i
         chk(hipMalloc(&d_best, n * sizeof(int32_t)), "hipMalloc: %s") &&
         (ns == 0 || chk(hipMemcpy(d_sub, subs.data(), (size_t)ns * sizeof(uint4), hipMemcpyHostToDevice), "H2D: %s")) &&
         chk(hipMemcpy(d_off, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice), "H2D: %s") &&
-        chk(hipMemsetAsync(c->d_ctl, 0, 64, nullptr), "hipMemset: %s")) {
+        chk(hipMemsetAsync(c->d_ctl, 0, CTL_BYTES, nullptr), "hipMemset: %s")) {
         if (ns) {
             KArgs a = make_args(c, nullptr, nullptr, (uint32_t)ns, false);
             a.prm.sw_window = window_size;
@@ -2280,7 +2503,7 @@ svt_status svt_load_insseq(svt_ctx *c, const svt_insseq_view *v) {
     if (v->n_ins && v->off[0] != 0) return fail(c, SVT_EINVAL, "insseq: %s", "off[0] != 0");
     for (uint64_t k = 0; k < v->n_ins; k++)
         if (v->off[k + 1] < v->off[k]) return fail(c, SVT_EINVAL, "insseq: %s", "off not monotone");
-    HIP_TRY(c, hipSetDevice(c->device));
+    DEV_GUARD(c);
     hfree(c->d_ins_off);
     hfree(c->d_ins_bases);
     c->insseq_loaded = false;
@@ -2308,7 +2531,7 @@ svt_status svt_poa_consensus(svt_ctx *c, const svt_poa_params *p, const svt_locu
         p->max_nodes < p->max_len || p->max_nodes > 65000 || p->support_radius < 0 || p->max_support < 1 ||
         p->match > 1000 || p->mismatch > 1000 || p->gap_open > 1000 || p->gap_ext > 1000)
         return fail(c, SVT_EINVAL, "%s", "poa params out of range");
-    HIP_TRY(c, hipSetDevice(c->device));
+    DEV_GUARD(c);
     return poa_run(c, p, loci, refined, n, cap, bases, res);
 }
 
@@ -2318,7 +2541,10 @@ uint64_t svt_poa_deferred(const svt_ctx *c) { return c ? c->poa_deferred : 0; }
 
 void svt_close(svt_ctx *c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    for (svt_ctx *d : c->subs) svt_close(d);
+    c->subs.clear();
+    DevGuard dg(c->device);
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     free_pileup(c);
     hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->poa_small.d); hfree(c->poa_big.d);
     delete c;

@@ -55,6 +55,7 @@ void audt_usage() {
     printf("    --device <num>                    First GPU index [Default: 0]\n");
     printf("    --devices <i,j,...>               Explicit GPU per shard (overrides --gpus/--device)\n");
     printf("    --batch <num>                     Records per GPU launch [Default: 1048576]\n");
+    printf("    --spill-bytes <num>               Initial candidate spill pool per GPU; grown on demand [Default: 67108864]\n");
 }
 
 struct Args {
@@ -93,7 +94,8 @@ Args parse_audt(int argc, char **argv) {
         {"consensus-interval", required_argument, nullptr, 9},
         {"consensus-min-count", required_argument, nullptr, 10}, {"help", no_argument, nullptr, 11},
         {"gpus", required_argument, nullptr, 20}, {"device", required_argument, nullptr, 21},
-        {"batch", required_argument, nullptr, 22}, {"devices", required_argument, nullptr, 23}, {nullptr, 0, nullptr, 0}};
+        {"batch", required_argument, nullptr, 22}, {"devices", required_argument, nullptr, 23},
+        {"spill-bytes", required_argument, nullptr, 24}, {nullptr, 0, nullptr, 0}};
     int opt, li;
     while ((opt = getopt_long(argc, argv, "b:v:o:t:h", opts, &li)) != -1) {
         switch (opt) {
@@ -112,6 +114,7 @@ Args parse_audt(int argc, char **argv) {
         case 20: a.gpus = atoi(optarg); break;
         case 21: a.device = atoi(optarg); break;
         case 22: a.batch = (size_t)strtoull(optarg, nullptr, 10); break;
+        case 24: a.prm.spill_bytes = (uint64_t)strtoull(optarg, nullptr, 10); break;
         case 23: {
             a.devices.clear();
             for (const char *p = optarg; *p;) {

@@ -36,6 +36,23 @@ def shard_rows(loci: np.ndarray, world: int, rank: int) -> np.ndarray:
     return genomic_order(loci)[b0:b1]
 
 
+def padded_rows(n_total: int, world: int) -> int:
+    """Rows per rank in the gather (every rank sends the same count)."""
+    return max(1, (n_total + world - 1) // world)
+
+
+def shard_workload(loci: np.ndarray, pileup, params, world: int, rank: int):
+    """(rows, shard loci in genomic order, the reads their queries can reach) of rank `rank`.
+
+    params: anything with wider_interval / median_interval / narrow_interval (Params)."""
+    from .pileup import halo_slice
+    rows = shard_rows(loci, world, rank)
+    sl = loci[rows]
+    if world == 1:
+        return rows, sl, pileup
+    return rows, sl, halo_slice(pileup, sl, params.wider_interval, params.median_interval, params.narrow_interval)
+
+
 def pack_records(rows: np.ndarray, local: np.ndarray, per: int) -> np.ndarray:
     """{vcf_index, start, end, pad} uint32 records, padded to `per` rows."""
     if len(rows) > per:
@@ -60,6 +77,47 @@ def unpack_records(recs: np.ndarray, n_total: int) -> np.ndarray:
     out["start"][idx] = real[:, 1]
     out["end"][idx] = real[:, 2]
     return out
+
+
+class PipelinedGather:
+    """Double-buffered gather of per-step record buffers to rank 0 (bench.py's N > 1 step).
+
+    `buffer(i)` hands out step i's buffer (waiting -- as a stream dependency on GPU backends --
+    for the gather that last read it), `submit(i)` starts its asynchronous gather, so the
+    gather of step i overlaps the refinement launch of step i + 1."""
+
+    def __init__(self, make_buf, world: int, rank: int, enabled: bool = True, group=None):
+        import torch
+        self.bufs = [make_buf(), make_buf()]
+        self.lists = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in self.bufs]
+        self.handles = [None, None]
+        self.enabled = enabled and world > 1
+        self.group = group
+
+    def buffer(self, i: int):
+        b = i % 2
+        if self.handles[b] is not None:
+            self.handles[b].wait()
+            self.handles[b] = None
+        return self.bufs[b]
+
+    def submit(self, i: int) -> None:
+        if self.enabled:
+            import torch.distributed as dist
+            b = i % 2
+            self.handles[b] = dist.gather(self.bufs[b], self.lists[b], dst=0, group=self.group, async_op=True)
+
+    def drain(self) -> None:
+        for b in range(2):
+            if self.handles[b] is not None:
+                self.handles[b].wait()
+                self.handles[b] = None
+
+    def gathered(self, i: int):
+        """Rank 0: the buffers every rank sent at step i (after drain()); else None."""
+        if not self.enabled:
+            return [self.bufs[i % 2]]
+        return self.lists[i % 2]
 
 
 def gather_results(rows: np.ndarray, local: np.ndarray, n_total: int, device=None,

@@ -51,16 +51,26 @@ class SvtError(RuntimeError):
 class Engine:
     """One GPU context (svt_ctx).  Use one Engine per process/GPU."""
 
-    def __init__(self, params: Params | None = None, device: int = -1):
+    def __init__(self, params: Params | None = None, device: int = -1, devices: list[int] | None = None):
+        """One context on `device` (-1 = current), or -- with `devices` -- one context over
+        several GPUs (svt_open_multi: the pileup is replicated, host batches are split)."""
         self.lib = load_engine()
         self.params = params or Params()
         self._cp = self.params.to_c()
         h = C.c_void_p()
-        rc = self.lib.svt_open(C.byref(self._cp), int(device), C.byref(h))
+        if devices is not None:
+            dv = (C.c_int * len(devices))(*devices)
+            rc = self.lib.svt_open_multi(C.byref(self._cp), len(devices), dv, C.byref(h))
+        else:
+            rc = self.lib.svt_open(C.byref(self._cp), int(device), C.byref(h))
         if rc != 0:
             raise SvtError(rc, "svt_open failed (no HIP device, or consensus_min_count < 1)")
         self._h = h
         self._pileup = None
+
+    @property
+    def n_devices(self) -> int:
+        return int(self.lib.svt_device_count(self._h))
 
     def _check(self, rc: int) -> None:
         if rc != 0:
@@ -82,6 +92,12 @@ class Engine:
         """Device pointers (e.g. torch tensor .data_ptr()) on a hipStream_t handle (int)."""
         self._check(self.lib.svt_refine_device(self._h, C.c_void_p(d_loci), n, C.c_void_p(d_out),
                                                C.c_void_p(stream or 0)))
+
+    def refine_device_records(self, d_loci: int, n: int, d_rec: int, d_index: int | None = None,
+                              index_base: int = 0, stream: int | None = None) -> None:
+        """As refine_device, writing RECORD_DTYPE gather records {index, start, end, 0}."""
+        self._check(self.lib.svt_refine_device_records(self._h, C.c_void_p(d_loci), n, C.c_void_p(d_index or 0),
+                                                       int(index_base), C.c_void_p(d_rec), C.c_void_p(stream or 0)))
 
     def sync(self, stream: int | None = None) -> None:
         self._check(self.lib.svt_sync(self._h, C.c_void_p(stream or 0)))

@@ -117,3 +117,50 @@ def test_halo_slice_is_exact(seed):
                                  prm.narrow_interval)
                 got = O.refine_batch(sub, loci[rows], prm)
                 np.testing.assert_array_equal(got.view(np.uint32), full[rows].view(np.uint32))
+
+
+def _bench_path_worker(rank, world, port, outdir):
+    """bench.py's N > 1 data path on gloo: shard_workload -> per-step 16-B records ->
+    PipelinedGather (double-buffered async gathers) -> unpack at rank 0."""
+    import torch
+    import torch.distributed as dist
+
+    import oracle_ffi as O
+    from svtrek_amd import Params, sim
+    from svtrek_amd._lib import RECORD_DTYPE
+    from svtrek_amd.distributed import PipelinedGather, pack_records, padded_rows, shard_workload
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = sim.generate(sim.SimConfig(seed=23, n_loci=211, n_targets=3, del_frac=0.5, coverage=10))
+    rows, sl, sub = shard_workload(r.loci, r.pileup, Params(), world, rank)
+    per = padded_rows(len(r.loci), world)
+    pg = PipelinedGather(lambda: torch.full((per * RECORD_DTYPE.itemsize // 4,), -1, dtype=torch.int32),
+                         world, rank)
+    local = O.refine_batch(sub, sl)
+    steps = 5
+    for i in range(steps):   # each step writes its records into the buffer the pipeline hands out
+        buf = pg.buffer(i)
+        buf.copy_(torch.from_numpy(pack_records(rows, local, per).view(np.int32).reshape(-1)))
+        pg.submit(i)
+    pg.drain()
+    if rank == 0:
+        recs = np.concatenate([p.numpy().view(np.uint32) for p in pg.gathered(steps - 1)])
+        np.save(os.path.join(outdir, "recs.npy"), recs)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_bench_shard_and_gather_path(tmp_path, world):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
+    mp.spawn(_bench_path_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    import oracle_ffi as O
+    from svtrek_amd import sim
+    r = sim.generate(sim.SimConfig(seed=23, n_loci=211, n_targets=3, del_frac=0.5, coverage=10))
+    recs = np.load(tmp_path / "recs.npy")
+    got = unpack_records(recs, len(r.loci))
+    np.testing.assert_array_equal(got.view(np.uint32), O.refine_batch(r.pileup, r.loci).view(np.uint32))

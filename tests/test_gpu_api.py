@@ -1,0 +1,124 @@
+"""C-ABI contract details through the HIP engine (include/svtrek_gpu.h): gather records,
+launch ordering across streams, multi-device contexts, device selection, and the event
+walk's work counters (the roofline's algorithmic bytes)."""
+import numpy as np
+import oracle_ffi as O
+import pytest
+import torch
+
+from svtrek_amd import Engine, Params, sim
+from svtrek_amd._lib import LOCUS_DTYPE, RECORD_DTYPE, RESULT_DTYPE
+
+pytestmark = pytest.mark.gpu
+
+
+def _workload(n_loci=3000, seed=61):
+    cfg = sim.SimConfig(seed=seed, n_targets=2, n_loci=n_loci, del_frac=0.5, coverage=25.0)
+    return sim.generate(cfg)
+
+
+def _same(got, want):
+    bad = np.nonzero((got["start"] != want["start"]) | (got["end"] != want["end"]))[0]
+    assert len(bad) == 0, f"{len(bad)} loci differ; first #{bad[0]}: {got[bad[0]]} vs {want[bad[0]]}"
+
+
+def test_records_output(engine_factory):
+    """svt_refine_device_records: {row index, start, end, 0} per locus, same results."""
+    r = _workload()
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    n = len(r.loci)
+    want = eng.refine(r.loci)
+    d_loci = torch.from_numpy(r.loci.view(np.uint8).copy()).cuda()
+    idx = np.random.default_rng(0).permutation(n).astype(np.uint32)
+    d_idx = torch.from_numpy(idx.view(np.int32)).cuda()
+    d_rec = torch.full((n * 4,), -1, dtype=torch.int32, device="cuda")
+    eng.refine_device_records(d_loci.data_ptr(), n, d_rec.data_ptr(), d_idx.data_ptr())
+    eng.sync()
+    rec = d_rec.cpu().numpy().view(RECORD_DTYPE)
+    assert np.array_equal(rec["index"], idx) and (rec["pad"] == 0).all()
+    _same(rec, want)
+    eng.refine_device_records(d_loci.data_ptr(), n, d_rec.data_ptr(), None, 1000)
+    eng.sync()
+    rec = d_rec.cpu().numpy().view(RECORD_DTYPE)
+    assert np.array_equal(rec["index"], np.arange(1000, 1000 + n, dtype=np.uint32))
+    _same(rec, want)
+
+
+def test_launches_on_two_streams_stay_ordered(engine_factory):
+    """Launches of one context on two streams share its spill pool: the context orders them
+    (a window with > 256 candidates spills in every launch here), so both stay exact."""
+    from fuzz import cluster_pileup
+    from svtrek_amd import make_loci
+    vals = [500000 + (i * 37) % 600 for i in range(2000)]
+    pl = cluster_pileup(vals)
+    eng = engine_factory()
+    eng.load_pileup(pl)
+    loci = make_loci([(2, 1, 500100 + k, 510000 + k) for k in range(64)] + [(1, 1, 500300, 500300)] * 8)
+    want = O.refine_batch(pl, loci)
+    d_loci = torch.from_numpy(loci.view(np.uint8).copy()).cuda()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.empty(len(loci) * 8, dtype=torch.uint8, device="cuda") for _ in range(6)]
+    for k, o in enumerate(outs):
+        eng.refine_device(d_loci.data_ptr(), len(loci), o.data_ptr(), (s1 if k % 2 else s2).cuda_stream)
+    eng.sync(s1.cuda_stream)
+    eng.sync(s2.cuda_stream)
+    torch.cuda.synchronize()
+    for o in outs:
+        _same(o.cpu().numpy().view(RESULT_DTYPE), want)
+
+
+def test_multi_device_context_splits_batches():
+    """svt_open_multi: the pileup is replicated, host batches are split into contiguous
+    slices, one per device, results in input order.  On a one-GPU box both contexts sit on
+    device 0 (independent contexts), which exercises the same split/merge path."""
+    ndev = torch.cuda.device_count()
+    devices = list(range(min(ndev, 4))) if ndev > 1 else [0, 0]
+    r = _workload(n_loci=2501, seed=62)
+    want = O.refine_batch(r.pileup, r.loci, threads=8)
+    with Engine(Params(), devices=devices) as eng:
+        assert eng.n_devices == len(devices)
+        eng.load_pileup(r.pileup)
+        _same(eng.refine(r.loci), want)
+        w = eng.count_work(r.loci)
+        _, ow = O.refine_batch(r.pileup, r.loci, threads=8, with_work=True)
+        assert (w["windows"], w["reads"], w["ops_walked"], w["candidates"]) == \
+            (ow["windows"], ow["reads"], ow["ops_walked"], ow["candidates"])
+        _same(eng.refine(r.loci[:3]), want[:3])   # fewer loci than devices
+
+
+def test_entry_points_restore_current_device(engine_factory):
+    """Every svt_* call selects its context's device and gives the thread its device back."""
+    r = _workload(n_loci=200, seed=63)
+    eng = engine_factory()
+    torch.cuda.set_device(0)
+    before = torch.cuda.current_device()
+    eng.load_pileup(r.pileup)
+    eng.refine(r.loci)
+    assert torch.cuda.current_device() == before
+
+
+def test_event_walk_counters(engine_factory):
+    """svt_work's event-walk counters: internally consistent and event_bytes = their sum at
+    the documented sizes; the counting launch's results equal the plain launch's."""
+    r = _workload(n_loci=4000, seed=64)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    w = eng.count_work(r.loci)
+    n = len(r.loci)
+    assert w["queries"] <= w["windows"] and w["queries"] > 0.9 * w["windows"]
+    assert w["range_reads"] >= w["reads"] > 0
+    assert w["probe_entries"] >= 2 * w["queries"] * 0.5
+    assert w["list_entries"] >= w["list_reads"]
+    assert w["stop_chunk_words"] >= w["stop_searches"]
+    exp = (24 * n + 32 * w["queries"] + 4 * w["probe_entries"] + 32 * w["reads"]
+           + 16 * (w["range_reads"] - w["reads"]) + 8 * w["list_reads"] + 8 * w["list_entries"]
+           + 36 * w["stop_searches"] + 4 * w["stop_chunk_words"])
+    assert w["event_bytes"] == exp
+    # the event walk reads far fewer bytes than the reference's CIGAR walk touches
+    assert w["event_bytes"] < 24 * n + 12 * w["reads"] + 4 * w["ops_walked"]
+    _same(eng.refine(r.loci), O.refine_batch(r.pileup, r.loci, threads=8))
+
+
+def test_locus_dtype_layout():
+    assert LOCUS_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 16

@@ -95,14 +95,34 @@ def test_spill_path(engine_factory):
     _assert_same(got, want, loci)
 
 
-def test_spill_pool_exhaustion_reported(engine_factory):
+def test_spill_pool_grows_on_demand(engine_factory):
+    """A 1 KiB pool cannot hold a 3000-candidate window: the synchronous call grows the pool
+    to what the launch asked for and re-runs (the reference reallocs its candidate arrays,
+    refinement.c:125-133), so the result is still exact; the asynchronous call reports
+    EOVERFLOW once through svt_sync, after which the same launch fits."""
+    import torch
+
+    from svtrek_amd import SvtError
+    from svtrek_amd._lib import RESULT_DTYPE
     vals = [400000 + i % 700 for i in range(3000)]
     pl = cluster_pileup(vals)
     eng = engine_factory(Params(spill_bytes=1024))
     eng.load_pileup(pl)
-    from svtrek_amd import SvtError
-    with pytest.raises(SvtError):
-        eng.refine(make_loci([(2, 1, 400100, 410000)]))
+    loci = make_loci([(2, 1, 400100, 410000), (1, 1, 400300, 400300)])
+    _assert_same(eng.refine(loci), O.refine_batch(pl, loci), loci)
+
+    eng2 = engine_factory(Params(spill_bytes=1024))
+    eng2.load_pileup(pl)
+    d_loci = torch.from_numpy(loci.view(np.uint8).copy()).cuda()
+    d_out = torch.empty(len(loci) * RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    eng2.refine_device(d_loci.data_ptr(), len(loci), d_out.data_ptr())
+    with pytest.raises(SvtError) as ei:
+        eng2.sync()
+    assert ei.value.code == -5
+    eng2.refine_device(d_loci.data_ptr(), len(loci), d_out.data_ptr())
+    eng2.sync()
+    got = d_out.cpu().numpy().view(RESULT_DTYPE)
+    _assert_same(got, O.refine_batch(pl, loci), loci)
 
 
 def test_long_cigars(engine_factory):

@@ -11,7 +11,7 @@ from svtrek_amd import sim
 pytestmark = pytest.mark.gpu
 
 
-def _check(engine_factory, cfg, threads=8):
+def _check(engine_factory, cfg, threads=16):
     r = sim.generate(cfg)
     eng = engine_factory()
     eng.load_pileup(r.pileup)
@@ -43,3 +43,27 @@ def test_cfg5_ultralong_subset(engine_factory):
     """60x ultra-long (50 kb, ~2000 ops/read): deep pileups, reads crossing several tiles."""
     cfg = replace(sim.WORKLOADS["cfg5_100k_60x_ul_ont"], n_loci=400, n_targets=1)
     _check(engine_factory, cfg)
+
+
+def test_cfg3_full_parity(engine_factory):
+    """BASELINE config 3 at full size: all 50k DEL+INS loci (16 oracle threads)."""
+    r, got = _check(engine_factory, sim.WORKLOADS["cfg3_50k_delins_30x_ont"])
+    assert len(got) == 50000
+
+
+def test_cfg4_full_parity(engine_factory):
+    """BASELINE config 4 at full size -- the bench's workload: all 1M loci over 22 contigs,
+    including the windows that spill past the LDS candidate buffer."""
+    cfg = sim.WORKLOADS["cfg4_1m_delins_30x_hifi"]
+    r = sim.generate(cfg)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    got = eng.refine(r.loci)
+    want, ow = O.refine_batch(r.pileup, r.loci, threads=16, with_work=True)
+    bad = np.nonzero((got["start"] != want["start"]) | (got["end"] != want["end"]))[0]
+    assert len(bad) == 0, f"{len(bad)} loci differ, first {r.loci[bad[0]]}: gpu {got[bad[0]]} oracle {want[bad[0]]}"
+    w = eng.count_work(r.loci)
+    assert (w["windows"], w["reads"], w["ops_walked"], w["candidates"]) == \
+        (ow["windows"], ow["reads"], ow["ops_walked"], ow["candidates"])
+    assert w["spilled_windows"] > 0          # the spill path ran at scale, and agreed
+    assert len(got) == 1_000_000
