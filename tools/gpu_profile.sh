@@ -18,13 +18,15 @@ step() {  # name, timeout, cmd...
   echo "[$(date +%T)] $name rc=$rc" >> "$OUT/steps.log"
   if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc"; tail -20 "$OUT/$name.log"; exit $rc; fi
 }
-B=(python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "${ARGS[@]}")
+B=(python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-cold "${ARGS[@]}")
 step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline "${ARGS[@]}"
+  python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-cold "${ARGS[@]}"
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- "${B[@]}"
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- "${B[@]}"
 step pmc_rdreq 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
   --output-format csv -d "$OUT/pmc_rdreq" -o run -- "${B[@]}"
 step pmc_dram 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
   --output-format csv -d "$OUT/pmc_dram" -o run -- "${B[@]}"
+step pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+  SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc_sq" -o run -- "${B[@]}"
 echo "profile $TAG done"

@@ -36,14 +36,15 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
     ap.add_argument("dst")
-    ap.add_argument("--workload", default="cfg2_10kdel_30x_ont")
+    ap.add_argument("--workload", default="cfg4_1m_delins_30x_hifi")
     ap.add_argument("--kernel", default="refine_event_kernel")
     a = ap.parse_args()
     os.makedirs(a.dst, exist_ok=True)
     copies = {"trace/run_kernel_stats.csv": "kernel_stats.csv", "pmc_fetch/run_counter_collection.csv":
               "pmc_fetch_size.csv", "pmc_write/run_counter_collection.csv": "pmc_write_size.csv",
               "pmc_rdreq/run_counter_collection.csv": "pmc_rdreq.csv",
-              "pmc_dram/run_counter_collection.csv": "pmc_dram.csv", "trace.log": "bench_under_rocprof.log"}
+              "pmc_dram/run_counter_collection.csv": "pmc_dram.csv", "pmc_sq/run_counter_collection.csv": "pmc_sq.csv",
+              "trace.log": "bench_under_rocprof.log"}
     for s, d in copies.items():
         if os.path.exists(os.path.join(a.src, s)):
             shutil.copy(os.path.join(a.src, s), os.path.join(a.dst, d))
@@ -67,6 +68,7 @@ def main() -> int:
         method_rd = "2 x FETCH_SIZE"
     out = {
         "kernel": a.kernel,
+        "records": True,   # bench.py's launches write 16-B gather records
         "workload": a.workload,
         "engine_version": ver,
         "read_bytes_per_launch": int(round(rd)),
@@ -81,8 +83,18 @@ def main() -> int:
                   "median over the profiled launches",
         "source": f"{a.dst}/pmc_*.csv",
     }
-    with open(os.path.join(os.path.dirname(a.dst.rstrip("/")), "traffic.json"), "w") as f:
-        json.dump(out, f, indent=1)
+    # profiles/traffic.json: one entry per (engine version, workload, kernel, records)
+    tpath = os.path.join(os.path.dirname(a.dst.rstrip("/")), "traffic.json")
+    try:
+        with open(tpath) as f:
+            old = json.load(f)
+        old = old if isinstance(old, list) else [old]
+    except (OSError, ValueError):
+        old = []
+    key = lambda e: (e.get("engine_version"), e.get("workload"), e.get("kernel"), bool(e.get("records")))  # noqa
+    entries = [e for e in old if key(e) != key(out)] + [out]
+    with open(tpath, "w") as f:
+        json.dump(entries, f, indent=1)
     print(json.dumps(out))
     return 0
 
