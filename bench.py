@@ -14,7 +14,7 @@ collective of the path: an RCCL gather to rank 0 of the slice's 16-B {vcf_index,
 pad} records, padded to ceil(N_total / N) rows; the gather of step i overlaps the launch of
 step i + 1 (double-buffered records).  Rank 0 prints ONE JSON line.
 
-roofline (the timed kernel, refine_event_kernel): `achieved` = the event walk's algorithmic
+roofline (the timed kernel, refine_span_kernel): `achieved` = the span walk's algorithmic
 bytes per launch (svt_work.event_bytes, counted exactly by svt_count_work; DESIGN.md
 "Roofline") / the kernel's mean launch time from HIP events on the launch stream.  `ref_walk`
 keeps SURVEY.md §8(d)'s figure (the bytes the reference's CIGAR walk touches) against index
@@ -282,7 +282,9 @@ def main() -> int:
     achieved = ev_bytes / (kern_mean_ms * 1e-3) / 1e9
     ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
     ref_ms = kern_mean_ms + load_stats["index_ms"]
-    kernel = "refine_event_kernel"
+    gather_variant = os.environ.get("SVTREK_GATHER", "span")
+    kernel = {"span": "refine_span_kernel", "event": "refine_event_kernel",
+              "index": "refine_index_kernel"}.get(gather_variant, "refine_kernel")
     traffic, traffic_src = _traffic(args.workload, kernel, records=True)
     if args.scale != 1.0 or world > 1:
         traffic = traffic_src = None
@@ -326,9 +328,10 @@ def main() -> int:
                          "kernel_ms_warm_min": round(warm_ms[0], 5),
                          "kernel_ms_cold": round(cold_ms, 5) if cold_ms else None,
                          "alg_bytes_per_launch": ev_bytes,
-                         "alg_bytes": "event walk: 36 B/locus (16 in, 4 row index, 16 record out) + 32 B/query + 4 B/search entry + 32 B/yielded read "
-                                      "+ 16 B/overlap-failing read in range + 8 B/list offset + 8 B/list entry "
-                                      "+ 36 B/stop search + 4 B/stop chunk word (svt_work)",
+                         "alg_bytes": ("span walk: 36 B/locus (16 in, 4 row index, 16 record out) + 32 B/query "
+                                       "+ 4 B/search entry + 16 B/span bounds + 16 B/span event + 36 B/stop search "
+                                       "+ 4 B/stop chunk word (svt_work)") if gather_variant == "span" else
+                                      f"{gather_variant} gather (svt_work.event_bytes)",
                          "ref_walk": {"bytes": ref_bytes, "ms": round(ref_ms, 5),
                                       "gbs": round(ref_bytes / (ref_ms * 1e-3) / 1e9, 2),
                                       "note": "SURVEY 8(d) bytes of the reference's CIGAR walk / (device index "

@@ -113,8 +113,8 @@ typedef struct svt_pileup_view {
 
 /* Work counters of one batch (svt_count_work).  The first group is what the reference
  * algorithm touches (24 B/locus + 12 B/yielded read + 4 B/CIGAR word
- * walked); the second is what the engine's event walk (refine_event_kernel) must read
- * for the same batch -- its algorithmic bytes are `event_bytes` (DESIGN.md "Roofline"). */
+ * walked); the others are what the engine's gather variant must read for the same batch --
+ * its algorithmic bytes are `event_bytes` (DESIGN.md "Roofline"). */
 typedef struct svt_work {
     uint64_t windows;        /* region queries issued (INV windows excluded)             */
     uint64_t reads;          /* reads yielded by the region queries                      */
@@ -122,7 +122,7 @@ typedef struct svt_work {
                                 plus the soft-clip test word when not already walked      */
     uint64_t candidates;     /* breakpoint candidates pushed                              */
     uint64_t spilled_windows;/* windows whose candidates exceeded SVT_LDS_CANDS          */
-    /* event walk (zero for the A/B gather variants) */
+    /* region query (event and span walks) + event walk (SVTREK_GATHER=event only) */
     uint64_t queries;        /* windows whose query reached the bucket table (32 B each)  */
     uint64_t probe_entries;  /* pos[]/emax[] entries the two searches need, boundary incl. */
     uint64_t range_reads;    /* reads in the query ranges [lo,hi): yielded (rec+rec2, 32 B)
@@ -132,8 +132,12 @@ typedef struct svt_work {
     uint64_t list_entries;   /* list entries read past the inline one (8 B each)          */
     uint64_t stop_searches;  /* refine_end break searches: 8 CIGAR words + 1 chunk word  */
     uint64_t stop_chunk_words; /* chunk-index words those searches scan, break chunk incl. */
-    uint64_t event_bytes;    /* algorithmic bytes of the batch's event walk (sum of the above
-                                at their byte sizes + 24 B per locus)                     */
+    /* span walk (the default gather; zero for the others) */
+    uint64_t span_bounds;    /* queries that read their span's two 8-B bounds             */
+    uint64_t span_events;    /* 16-B events in the queries' spans                         */
+    uint64_t event_bytes;    /* algorithmic bytes of the batch under the context's gather
+                                variant: 24 B per locus + its reads at their byte sizes
+                                (DESIGN.md "Roofline")                                    */
 } svt_work;
 
 /* One refined call as the multi-GPU gather moves it: the record's index

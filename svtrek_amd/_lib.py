@@ -81,6 +81,8 @@ class SvtWork(C.Structure):
         ("list_entries", C.c_uint64),
         ("stop_searches", C.c_uint64),
         ("stop_chunk_words", C.c_uint64),
+        ("span_bounds", C.c_uint64),
+        ("span_events", C.c_uint64),
         ("event_bytes", C.c_uint64),
     ]
 

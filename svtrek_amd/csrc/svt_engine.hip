@@ -23,6 +23,7 @@
 // (walk_read) that replays the reference's uint32 arithmetic op by op.  No floating
 // point, no MFMA: integer scan + vote, HBM-streaming bound.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <stdint.h>
 #include <stdio.h>
@@ -37,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.8.8 (gfx950, event walk)"
+#define SVT_VERSION "svtrek_amd 0.9.0 (gfx950, span walk)"
 
 namespace {
 
@@ -63,6 +64,14 @@ constexpr uint32_t CH_DEL = 1u << 30;       //   the chunk holds a D op with len
 constexpr uint32_t CH_INS = 1u << 31;       //   the chunk holds an I op with len >= 50 (refinement.c:299)
 constexpr uint32_t CHUNK_PAD = 1040;        // zero words after the chunk index (speculative tile over-read)
 constexpr uint64_t INDEX_LIMIT = 1ull << 29; // walks reaching 2^29 are flagged slow (chunk word has 29 position bits)
+constexpr uint64_t WALK_LIMIT = 1ull << 28;  // ... and so are walks of 2^28 bases or more (a span event's 28-bit field)
+// Span events (svt_load_pileup, span_kernel): every read's breakpoint events, 16 B each,
+// self-contained {x, w, endpos, aux} so that a window is one filter over a contiguous span:
+//   D list: D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:190),
+//           SP_LEAD {pos, walk << 4 | SP_LEAD, endpos, arena offset low 32} for cigar[0] == S (:210),
+//           SP_TRAIL {walk end, SP_TRAIL, endpos, 0} for cigar[n-1] == S (:120,:147);
+//   I list: I >= 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:299).
+constexpr uint32_t SP_TRAIL = 0xEu, SP_LEAD = 0xFu;   // op codes no candidate event carries
 
 struct DevPileup {
     const int32_t *pos;       // [n_reads]
@@ -77,6 +86,11 @@ struct DevPileup {
     const uint4 *rec2;        // [n_reads] {walk end, candidate-op count, first candidate op (ev[evoff[r]])}
     const uint64_t *evoff;    // [n_reads] offset of the read's candidate ops in ev
     const uint2 *ev;          // candidate ops of every read in op order: {walk position before the op, CIGAR word}
+    const uint64_t *spoffD;   // [n_reads+1] span events: read r's D-list events are spD[spoffD[r] .. spoffD[r+1])
+    const uint64_t *spoffI;   // [n_reads+1]              its I-list events spI[spoffI[r] .. spoffI[r+1])
+    const uint4 *spD;
+    const uint4 *spI;
+    const uint64_t *slowpre;  // [n_reads+1] slow reads before read r (their walks take walk_read)
     int32_t n_targets;
 };
 
@@ -106,7 +120,8 @@ struct KArgs {
 
 // svt_work counter slots (refine_window's wk[], the context's work words)
 constexpr int W_WINDOWS = 0, W_READS = 1, W_OPS = 2, W_CANDS = 3, W_SPILLED = 4, W_QUERIES = 5, W_PROBE = 6,
-              W_RANGE = 7, W_LREADS = 8, W_LENTRIES = 9, W_STOPS = 10, W_STOPCH = 11, W_N = 12;
+              W_RANGE = 7, W_LREADS = 8, W_LENTRIES = 9, W_STOPS = 10, W_STOPCH = 11, W_SQUERIES = 12,
+              W_SPAN = 13, W_N = 14;
 constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status, work counters
 static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
 
@@ -227,6 +242,7 @@ struct WinStats {
     unsigned long long reads = 0, ops = 0;
     // event walk's own reads (G_EVENT COUNT builds): see svt_work
     unsigned long long queries = 0, probe = 0, range = 0, lreads = 0, lentries = 0, stops = 0, stopch = 0;
+    unsigned long long squeries = 0, span = 0;   // span walk (G_SPAN COUNT builds)
 };
 
 template <int KIND>
@@ -1095,6 +1111,133 @@ __device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32
     if (COUNT) st.ops += rdlane(live_ops, 0);
 }
 
+// ------------------------------------------------------------------ span walk (default)
+// The reads [lo, hi) of a window own one contiguous span of the D (or I) event list, and
+// every event carries what its tests need (its read's endpos for the overlap test of
+// hts_itr_next), so a window is: region query, the span's two bounds, then ONE filter over
+// the span, every load of a 256-event batch issued at once (no per-read dependent chain).
+// An op is processed by the reference walk iff the walk position before it is <= inter.end
+// (positions only grow along a read, refinement.c:145), so a candidate event counts iff
+// x <= e; the soft-clip events follow refinement.c:147-159 (trailing S: no break, s <= walk
+// end <= e) and :210-220 (leading S, s <= pos <= e: walk end + 1, or the position after the
+// break op + 1 -- found by stop_rows in the chunk index).
+constexpr int SPAN_U = 4;   // 16-B event loads in flight per lane
+
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The span walk's own reads, for svt_count_work: the two span bounds, the events of the
+// span, and per leading-S stop the chunk words scanned to the break chunk.
+template <int KIND>
+__device__ __forceinline__ void span_count(const DevPileup &P, int tid, uint32_t s, uint32_t e, WinStats &st) {
+    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
+    int64_t lo, hi;
+    if (!read_range(P, tid, beg, end, lo, hi, &st)) return;
+    const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
+    const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
+    const uint64_t E0 = off[lo], E1 = off[hi];
+    st.squeries++;
+    st.span += E1 - E0;
+    if (KIND != K_END) return;
+    const uint64_t cbase = P.off64[P.tid_off[tid]];
+    for (uint64_t b = E0; b < E1; b += WAVE) {
+        const uint64_t j = b + (uint64_t)lane_id();
+        const uint4 v = j < E1 ? ev[j] : make_uint4(0, 0, 0, 0);
+        const bool brk = (v.y & 0xfu) == SP_LEAD && (int64_t)(int32_t)v.z > beg && s <= v.x && v.x <= e &&
+                         v.x + (v.y >> 4) > e;
+        uint64_t m = ballot(brk);
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t offlo = rdlane(v.w, l);
+            uint32_t bi;
+            (void)break_after(P, cbase + (uint64_t)(offlo - (uint32_t)cbase), NCIG_MASK, rdlane(v.x, l), e, bi);
+            st.stops++;
+            st.stopch += (unsigned long long)(bi / CHUNK + 1u);
+        }
+    }
+}
+
+template <int KIND, bool COUNT>
+__device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
+                                            WinStats &st) {
+    if (COUNT) {   // diagnostic: the reference's work by the exact per-read walk + what the span walk reads
+        gather_perread<KIND, true>(P, tid, s, e, sink, st);
+        if (e < 0x80000000u) span_count<KIND>(P, tid, s, e, st);
+        return;
+    }
+    // Event positions are walk positions < 2^29 (longer walks are flagged slow at load time
+    // and carry no events); windows ending at or past 2^31 take the exact per-read path.
+    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
+    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
+    int64_t lo, hi;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
+    const int ln = lane_id();
+    const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
+    const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
+    // one step: the span bounds (lanes 0, 1) and the slow-read count of [lo, hi) (lanes 2, 3)
+    const uint64_t ob = ln < 2 ? off[ln ? hi : lo] : ln < 4 ? P.slowpre[ln == 3 ? hi : lo] : 0ull;
+    const uint64_t cbase = KIND == K_END ? P.off64[P.tid_off[tid]] : 0ull;   // stop searches' arena base
+    const uint64_t E0 = rdlane64(ob, 0), E1 = rdlane64(ob, 1), nslow = rdlane64(ob, 3) - rdlane64(ob, 2);
+    int32_t cnt = 0;   // candidates appended so far (wave-uniform)
+    for (uint64_t b = E0; b < E1; b += SPAN_U * WAVE) {
+        uint4 v[SPAN_U];
+#pragma unroll
+        for (int u = 0; u < SPAN_U; u++) {
+            const uint64_t j = b + (uint64_t)(u * WAVE + ln);
+            v[u] = j < E1 ? ev[j] : make_uint4(0, 0, 0, 0);   // zero event: op M, endpos 0 -> no candidate
+        }
+#pragma unroll
+        for (int u = 0; u < SPAN_U; u++) {
+            const uint32_t x = v[u].x, op = v[u].y & 0xfu, len = v[u].y >> 4;
+            const bool ovl = (int64_t)(int32_t)v[u].z > beg;   // hts_itr_next overlap; pos < end holds below hi
+            bool c, brk = false;
+            uint32_t val = x;
+            if (KIND == K_INS) {
+                c = ovl && op == OP_INS && x <= e;                                      // refinement.c:299
+            } else if (KIND == K_START) {
+                c = ovl && x <= e && (op == OP_DEL || (op == SP_TRAIL && s <= x));      // :124 / :147-159
+            } else {
+                const bool lead = op == SP_LEAD && ovl && s <= x && x <= e;            // :210-220
+                const uint32_t wend = x + len;
+                brk = lead && wend > e;
+                c = (ovl && x <= e && op == OP_DEL) || (lead && !brk);                  // :190-200
+                val = op == OP_DEL ? x + len + 1u : wend + 1u;
+            }
+            const uint64_t m = ballot(c);
+            const int32_t idx = cnt + (int32_t)mbcnt(m);
+            if (c && idx < sink.cap) sink.buf[idx] = (int32_t)val;
+            cnt += (int32_t)__popcll(m);
+            if (KIND == K_END) {
+                uint64_t sm = ballot(brk);
+                if (sm) {   // the position after the break op, rare: the sink's LDS counter takes over
+                    if (ln == 0) *sink.cnt = cnt;
+                    wave_sync();
+                    while (sm) sm = stop_rows(P, cbase, sm, NCIG_MASK, x, v[u].w, e, sink);
+                    wave_sync();
+                    cnt = uniform_i(*sink.cnt);
+                }
+            }
+        }
+    }
+    if (ln == 0) *sink.cnt = cnt;
+    if (nslow) {   // reads whose walk could leave the event range: exact per-read replay (never in practice)
+        wave_sync();
+        for (int64_t rb = lo; rb < hi; rb += WAVE) {
+            const int64_t r = rb + ln;
+            const uint4 rc = r < hi ? P.rec[r] : make_uint4(0, 0, 0, 0);
+            uint64_t sm = ballot((rc.z & SLOW_BIT) && (int64_t)(int32_t)rc.y > beg);
+            while (sm) {
+                const int l = __builtin_ctzll(sm);
+                sm &= sm - 1;
+                const uint32_t z = rdlane(rc.z, l);
+                walk_read<KIND, false>(P.cigar, P.off64[rb + l], z & NCIG_MASK, rdlane(rc.x, l), z >> 30, s, e, sink, st);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ sort + vote (A8-A10)
 // Bitonic sort of buf[0..N) (N power of two, padded with INT32_MAX) by one wave.
 __device__ __forceinline__ void wave_bitonic_sort(int32_t *buf, int N) {
@@ -1378,14 +1521,15 @@ struct WinLds {
     int32_t ncand;
 };
 
-constexpr int G_PERREAD = 0, G_STREAM = 1, G_INDEX = 2, G_EVENT = 3;   // window gather variants (SVTREK_GATHER)
+constexpr int G_PERREAD = 0, G_STREAM = 1, G_INDEX = 2, G_EVENT = 3, G_SPAN = 4;   // window gather variants (SVTREK_GATHER)
 
 template <int KIND, bool COUNT, int G>
 __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
                                           WinLds &L) {
     if (lane_id() == 0) *sink.cnt = 0;
     wave_sync();
-    if (G == G_EVENT) gather_event<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    if (G == G_SPAN) gather_span<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    else if (G == G_EVENT) gather_event<KIND, COUNT>(a.pile, tid, s, e, sink, st);
     else if (G == G_INDEX) gather_index<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.il);
     else if (G == G_STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.sl);
     else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
@@ -1403,6 +1547,7 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
         wk[W_WINDOWS] += 1; wk[W_READS] += st.reads; wk[W_OPS] += st.ops; wk[W_CANDS] += (unsigned long long)n;
         wk[W_QUERIES] += st.queries; wk[W_PROBE] += st.probe; wk[W_RANGE] += st.range; wk[W_LREADS] += st.lreads;
         wk[W_LENTRIES] += st.lentries; wk[W_STOPS] += st.stops; wk[W_STOPCH] += st.stopch;
+        wk[W_SQUERIES] += st.squeries; wk[W_SPAN] += st.span;
     }
     support = 0;
     if (n < a.prm.min_count) return -1;                    // refinement.c:43-45 (sliding: no support >= min_count)
@@ -1483,6 +1628,7 @@ __global__ __launch_bounds__(64 * WPB) void refine_kernel(KArgs a) { refine_body
 
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_index_kernel(KArgs a) { refine_body<false, G_INDEX>(a); }
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_event_kernel(KArgs a) { refine_body<false, G_EVENT>(a); }
+__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_span_kernel(KArgs a) { refine_body<false, G_SPAN>(a); }
 
 template <bool COUNT, int G>
 __device__ __forceinline__ void refine_body(const KArgs &a) {
@@ -1579,7 +1725,8 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ raw, const uint64_t *__restrict__ raw_off,
                                                    const uint64_t *__restrict__ poff, uint4 *rec,
                                                    uint32_t *__restrict__ arena, uint32_t *__restrict__ chunk,
-                                                   uint4 *__restrict__ rec2, uint32_t *__restrict__ nev_out, int64_t nr) {
+                                                   uint4 *__restrict__ rec2, uint64_t *__restrict__ cnt, int64_t S,
+                                                   int64_t nr) {
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= nr) return;
     const int ln = lane_id();
@@ -1624,11 +1771,64 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ 
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) walk += __shfl_xor(walk, d, WAVE);
     if (ln == 0) {
-        if ((uint64_t)rpos + walk >= INDEX_LIMIT) rec[r].z |= SLOW_BIT;
+        const uint32_t z = rec[r].z;
+        const bool slow = (uint64_t)rpos + walk >= INDEX_LIMIT || walk >= WALK_LIMIT;
+        if (slow) rec[r].z = z | SLOW_BIT;
         rec2[r] = make_uint4(rpos + (uint32_t)walk, nev, 0u, 0u);
-        nev_out[r] = nev;         // candidate ops (D > 50 or I >= 50)
-        nev_out[nr + r] = nins;   // I >= 50 ops (the allele-consensus sequences, svt_load_insseq)
+        // per-read counts, one array of stride S = n_reads + 1 each (exclusive scans -> offsets)
+        cnt[r] = nev;                                  // candidate ops (D > 50 or I >= 50): event lists
+        cnt[S + r] = nins;                             // I >= 50 ops (allele-consensus sequences, svt_load_insseq)
+        cnt[2 * S + r] = slow ? 0u : nev - nins + (uint32_t)__popc(z >> 30);   // span D list (+ soft-clip events)
+        cnt[3 * S + r] = slow ? 0u : nins;                                    // span I list
+        cnt[4 * S + r] = slow ? 1u : 0u;                                     // slow reads (exact per-read walk)
     }
+}
+
+// Span events of every read (see SP_TRAIL / SP_LEAD): its D list at spoffD[r], I list at
+// spoffI[r], candidate ops in op order with the walk position before each (refinement.c:141).
+// Slow reads own no events (pack_kernel counted none for them).
+__global__ __launch_bounds__(256) void span_kernel(const uint32_t *__restrict__ arena, const uint64_t *__restrict__ poff,
+                                                   const uint4 *__restrict__ rec, const uint4 *__restrict__ rec2,
+                                                   const uint64_t *__restrict__ spoffD, const uint64_t *__restrict__ spoffI,
+                                                   uint4 *__restrict__ spD, uint4 *__restrict__ spI, int64_t nr) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nr) return;
+    const int ln = lane_id();
+    uint64_t kD = spoffD[r], kI = spoffI[r];
+    if (spoffD[r + 1] == kD && spoffI[r + 1] == kI) return;
+    const uint4 rc = rec[r];
+    const uint64_t n = rc.z & NCIG_MASK, src = poff[r];
+    const uint32_t clip = rc.z >> 30, rpos = rc.x, endp = rc.y, wend = rec2[r].x;
+    if (clip & SVT_CLIP_FIRST_S) {   // refinement.c:210-220: cigar[0] == S
+        if (ln == 0) spD[kD] = make_uint4(rpos, ((wend - rpos) << 4) | SP_LEAD, endp, (uint32_t)src);
+        kD++;
+    }
+    uint32_t carry = rpos;
+    constexpr int SP_UN = 4;   // as pack_kernel: SP_UN loads in flight per wave
+    for (uint64_t b0 = 0; b0 < n; b0 += SP_UN * WAVE) {
+        uint32_t wv[SP_UN];
+#pragma unroll
+        for (int u = 0; u < SP_UN; u++) {
+            const uint64_t i = b0 + (uint64_t)(u * WAVE + ln);
+            wv[u] = i < n ? arena[src + i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < SP_UN; u++) {
+            if (b0 + (uint64_t)(u * WAVE) >= n) break;
+            const uint32_t w = wv[u];
+            const uint32_t adv = ref_adv(w);
+            const uint32_t after = carry + wave_scan_add(adv);
+            const bool d = is_candidate_op<K_START>(w & 0xfu, w >> 4), ins = is_candidate_op<K_INS>(w & 0xfu, w >> 4);
+            const uint64_t md = ballot(d), mi = ballot(ins);
+            const uint4 ev = make_uint4(after - adv, w, endp, 0u);
+            if (d) spD[kD + mbcnt(md)] = ev;
+            if (ins) spI[kI + mbcnt(mi)] = ev;
+            kD += (uint64_t)__popcll(md);
+            kI += (uint64_t)__popcll(mi);
+            carry = rdlane(after, WAVE - 1);
+        }
+    }
+    if ((clip & SVT_CLIP_LAST_S) && ln == 0) spD[kD] = make_uint4(wend, SP_TRAIL, endp, 0u);   // :120,:147-159
 }
 
 // Second load pass: every read's candidate ops (D > 50 or I >= 50, refinement.c:124,:190,:299)
@@ -1682,7 +1882,7 @@ __global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__
 struct svt_ctx {
     svt_params prm{};
     int device = 0;
-    int gather = G_EVENT;         // SVTREK_GATHER=index / stream / perread select the A/B variants
+    int gather = G_SPAN;          // SVTREK_GATHER=event / index / stream / perread select the A/B variants
     char err[512] = {0};
     // pileup
     int32_t n_targets = 0;
@@ -1706,6 +1906,8 @@ struct svt_ctx {
     PoaPool poa_small, poa_big;       // POA scratch slots (poa_pool)
     uint64_t poa_deferred = 0;        // loci the last svt_poa_consensus reran on full-size slots
     uint2 *d_ev = nullptr;
+    uint64_t *d_spoffD = nullptr, *d_spoffI = nullptr, *d_slowpre = nullptr;   // span walk
+    uint4 *d_spD = nullptr, *d_spI = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
     svt_load_stats load_stats{};      // timings of the last svt_load_pileup
@@ -1800,6 +2002,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar); hfree(c->d_chunk);
     hfree(c->d_rec2); hfree(c->d_evoff); hfree(c->d_ev); hfree(c->d_insbase); hfree(c->d_ins_off);
     hfree(c->d_ins_bases);
+    hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0;
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
@@ -1807,7 +2010,8 @@ void free_pileup(svt_ctx *c) {
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
-                       c->d_cigar, c->d_chunk, c->d_rec2, c->d_evoff, c->d_ev, c->n_targets};
+                       c->d_cigar, c->d_chunk, c->d_rec2, c->d_evoff, c->d_ev, c->d_spoffD, c->d_spoffI,
+                       c->d_spD, c->d_spI, c->d_slowpre, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
                     c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
     a.loci = d_loci;
@@ -1844,7 +2048,10 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     a.rec_index = rec_index;
     a.rec_base = rec_base;
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
-    if (c->gather == G_EVENT) {
+    if (c->gather == G_SPAN) {
+        if (count) hipLaunchKernelGGL((refine_kernel<true, G_SPAN>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
+    } else if (c->gather == G_EVENT) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_EVENT>), grid, block, 0, st, a);
         else hipLaunchKernelGGL(refine_event_kernel, grid, block, 0, st, a);
     } else if (c->gather == G_INDEX) {
@@ -2039,11 +2246,12 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     if (!c) return SVT_ENOMEM;
     c->prm = *params;
     const char *g = getenv("SVTREK_GATHER");
-    c->gather = !g ? G_EVENT
+    c->gather = !g ? G_SPAN
                 : strcmp(g, "perread") == 0 ? G_PERREAD
                 : strcmp(g, "stream") == 0  ? G_STREAM
                 : strcmp(g, "index") == 0   ? G_INDEX
-                                            : G_EVENT;
+                : strcmp(g, "event") == 0   ? G_EVENT
+                                            : G_SPAN;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;
@@ -2181,73 +2389,102 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload<uint32_t>(c, c->d_chunk, nullptr, 0, (size_t)(pw / CHUNK) + CHUNK_PAD))) return s;
     if ((s = upload<uint4>(c, c->d_rec2, nullptr, 0, (size_t)std::max<int64_t>(nr, 1)))) return s;
     if (nr > 0) {
-        // pass 1 (pack_kernel): padded arena, chunk index, walk ends, candidate-op counts;
-        // host: exclusive scan of the counts; pass 2 (event_kernel): the candidate-op lists
-        uint32_t *d_raw = nullptr, *d_nev = nullptr;
-        uint64_t *d_raw_off = nullptr;
-        std::vector<uint32_t> nev((size_t)nr * 2);
-        std::vector<uint64_t> evoff((size_t)nr + 1, 0);
+        // pass 1 (pack_kernel): padded arena, chunk index, walk ends, per-read counts; device
+        // exclusive scans of the counts; pass 2: the gather variant's lists (event_kernel for
+        // the event walk, span_kernel for the span walk).  Only the scan totals come back.
+        const size_t S = (size_t)nr + 1;   // count-array stride: n_reads counts + a zero
+        uint32_t *d_raw = nullptr;
+        uint64_t *d_raw_off = nullptr, *d_cnt = nullptr;
+        void *d_tmp = nullptr;
+        size_t tmp_bytes = 0;
         hipError_t e = hipMalloc(&d_raw, std::max<uint64_t>(nops, 1) * 4);
-        if (e == hipSuccess) e = hipMalloc(&d_raw_off, ((size_t)nr + 1) * 8);
-        if (e == hipSuccess) e = hipMalloc(&d_nev, (size_t)nr * 8);
-        if (e == hipSuccess) e = hipMalloc(&c->d_evoff, ((size_t)nr + 1) * 8);
+        if (e == hipSuccess) e = hipMalloc(&d_raw_off, S * 8);
+        if (e == hipSuccess) e = hipMalloc(&d_cnt, 5 * S * 8);
+        if (e == hipSuccess) e = hipMemset(d_cnt, 0, 5 * S * 8);
         if (e == hipSuccess && nops) e = hipMemcpy(d_raw, p->cigar, nops * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, S * 8, hipMemcpyHostToDevice);
         c->load_stats.upload_ms = ms_since(t_up);
-        hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-        for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        for (int k = 0; k < 2 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
         if (e == hipSuccess) e = hipEventRecord(ev[0], nullptr);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, d_raw, d_raw_off,
-                               c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, c->d_rec2, d_nev, (int64_t)nr);
+                               c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, c->d_rec2, d_cnt, (int64_t)S, (int64_t)nr);
             e = hipGetLastError();
         }
-        if (e == hipSuccess) e = hipEventRecord(ev[1], nullptr);
-        if (e == hipSuccess) e = hipMemcpy(nev.data(), d_nev, (size_t)nr * 8, hipMemcpyDeviceToHost);
+        // out[0 .. S) = exclusive prefix sums of cnt[k*S .. k*S + S); returns out[S-1] (the total)
+        auto scan = [&](int k, uint64_t *&out, uint64_t &total) {
+            if (e != hipSuccess) return;
+            e = hipMalloc(&out, S * 8);
+            if (e != hipSuccess) return;
+            c->dev_bytes += S * 8;
+            size_t need = 0;
+            e = hipcub::DeviceScan::ExclusiveSum(nullptr, need, d_cnt + (size_t)k * S, out, (int)S, nullptr);
+            if (e == hipSuccess && need > tmp_bytes) {
+                hfree(d_tmp);
+                e = hipMalloc(&d_tmp, need);
+                tmp_bytes = e == hipSuccess ? need : 0;
+            }
+            if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_cnt + (size_t)k * S, out, (int)S,
+                                                                     nullptr);
+            if (e == hipSuccess) e = hipMemcpy(&total, out + (S - 1), 8, hipMemcpyDeviceToHost);
+        };
+        if (S > 0x7fffffffull) e = hipErrorInvalidValue;   // hipcub item count is an int
+        // each read's first I >= 50 op in the pileup-wide (read, op) order of the allele-consensus
+        // sequences (svt_load_insseq), and the slow-read prefix counts
+        uint64_t n_slow = 0, n_ev = 0, nD = 0, nI = 0;
+        scan(1, c->d_insbase, c->n_ins);
+        scan(4, c->d_slowpre, n_slow);
         hfree(d_raw);
         hfree(d_raw_off);
-        hfree(d_nev);
-        if (e == hipSuccess) {
-            for (int64_t r = 0; r < nr; r++) evoff[(size_t)r + 1] = evoff[(size_t)r] + nev[(size_t)r];
-            // each read's first I >= 50 op in the pileup-wide (read, op) order of the
-            // allele-consensus sequences (svt_load_insseq)
-            std::vector<uint64_t> ib((size_t)nr);
-            uint64_t acc = 0;
-            for (int64_t r = 0; r < nr; r++) { ib[(size_t)r] = acc; acc += nev[(size_t)nr + (size_t)r]; }
-            c->n_ins = acc;
-            e = hipMalloc(&c->d_insbase, (size_t)nr * 8);
-            if (e == hipSuccess) e = hipMemcpy(c->d_insbase, ib.data(), (size_t)nr * 8, hipMemcpyHostToDevice);
-            if (e == hipSuccess) c->dev_bytes += (size_t)nr * 8;
-        }
-        if (e == hipSuccess) {
-            e = hipMemcpy(c->d_evoff, evoff.data(), ((size_t)nr + 1) * 8, hipMemcpyHostToDevice);
-            c->dev_bytes += ((size_t)nr + 1) * 8;
-        }
-        if (e == hipSuccess) e = hipMalloc(&c->d_ev, std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2));
-        if (e == hipSuccess) {
-            c->dev_bytes += std::max<uint64_t>(evoff[(size_t)nr], 1) * sizeof(uint2);
-            e = hipEventRecord(ev[2], nullptr);
+        if (c->gather == G_EVENT) {
+            scan(0, c->d_evoff, n_ev);
+            if (e == hipSuccess) e = hipMalloc(&c->d_ev, std::max<uint64_t>(n_ev, 1) * sizeof(uint2));
             if (e == hipSuccess) {
+                c->dev_bytes += std::max<uint64_t>(n_ev, 1) * sizeof(uint2);
                 hipLaunchKernelGGL(event_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
                                    c->d_off64, c->d_rec, c->d_rec2, c->d_evoff, c->d_ev, (int64_t)nr);
                 e = hipGetLastError();
             }
-            if (e == hipSuccess) e = hipEventRecord(ev[3], nullptr);
         }
+        if (c->gather == G_SPAN) {
+            scan(2, c->d_spoffD, nD);
+            scan(3, c->d_spoffI, nI);
+            if (e == hipSuccess) e = hipMalloc(&c->d_spD, std::max<uint64_t>(nD, 1) * sizeof(uint4));
+            if (e == hipSuccess) e = hipMalloc(&c->d_spI, std::max<uint64_t>(nI, 1) * sizeof(uint4));
+            if (e == hipSuccess) {
+                c->dev_bytes += (std::max<uint64_t>(nD, 1) + std::max<uint64_t>(nI, 1)) * sizeof(uint4);
+                hipLaunchKernelGGL(span_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
+                                   c->d_off64, c->d_rec, c->d_rec2, c->d_spoffD, c->d_spoffI, c->d_spD, c->d_spI,
+                                   (int64_t)nr);
+                e = hipGetLastError();
+            }
+        }
+        if (e == hipSuccess) e = hipEventRecord(ev[1], nullptr);
         if (e == hipSuccess) e = hipDeviceSynchronize();
         if (e == hipSuccess) {
-            float a = 0.f, b = 0.f;
+            float a = 0.f;
             e = hipEventElapsedTime(&a, ev[0], ev[1]);
-            if (e == hipSuccess) e = hipEventElapsedTime(&b, ev[2], ev[3]);
-            c->load_stats.index_ms = (double)a + (double)b;
+            c->load_stats.index_ms = (double)a;
         }
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < 2; k++)
             if (ev[k]) (void)hipEventDestroy(ev[k]);
-        if (e != hipSuccess) return fail(c, SVT_EDEVICE, "pileup pack: %s", hipGetErrorString(e));
+        hfree(d_cnt);
+        hfree(d_tmp);
+        hfree(d_raw);
+        hfree(d_raw_off);
+        if (e != hipSuccess) return fail(c, SVT_EDEVICE, "pileup index: %s", hipGetErrorString(e));
     } else {
-        if ((s = upload<uint2>(c, c->d_ev, nullptr, 0, 1))) return s;
-        if ((s = upload<uint64_t>(c, c->d_evoff, nullptr, 0, 1))) return s;
+        if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, 1))) return s;
+        if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, 1))) return s;
     }
+    // variant arrays the pileup did not need: one zero element each (kernels never read them)
+    if (!c->d_ev && (s = upload<uint2>(c, c->d_ev, nullptr, 0, 1))) return s;
+    if (!c->d_evoff && (s = upload<uint64_t>(c, c->d_evoff, nullptr, 0, 1))) return s;
+    if (!c->d_spD && (s = upload<uint4>(c, c->d_spD, nullptr, 0, 1))) return s;
+    if (!c->d_spI && (s = upload<uint4>(c, c->d_spI, nullptr, 0, 1))) return s;
+    if (!c->d_spoffD && (s = upload<uint64_t>(c, c->d_spoffD, nullptr, 0, 1))) return s;
+    if (!c->d_spoffI && (s = upload<uint64_t>(c, c->d_spoffI, nullptr, 0, 1))) return s;
     c->n_targets = nt;
     c->n_reads = nr;
     c->n_ops = nops;
@@ -2354,13 +2591,22 @@ static svt_status run_batch_1(svt_ctx *c, const svt_locus *loci, size_t n, svt_r
         w->spilled_windows = k[W_SPILLED]; w->queries = k[W_QUERIES]; w->probe_entries = k[W_PROBE];
         w->range_reads = k[W_RANGE]; w->list_reads = k[W_LREADS]; w->list_entries = k[W_LENTRIES];
         w->stop_searches = k[W_STOPS]; w->stop_chunk_words = k[W_STOPCH];
-        // the event walk's algorithmic bytes (DESIGN.md "Roofline"): locus in + result out,
-        // two bucket words per search, the search entries, rec + rec2 of every yielded read and
-        // rec of every overlap-failing one in range, list offsets and entries, and per stop
-        // search the chunk words scanned, the word before the break chunk and its 8 CIGAR words
-        w->event_bytes = 24ull * n + 32ull * w->queries + 4ull * w->probe_entries + 32ull * w->reads +
-                         16ull * (w->range_reads - std::min(w->range_reads, w->reads)) + 8ull * w->list_reads +
-                         8ull * w->list_entries + 36ull * w->stop_searches + 4ull * w->stop_chunk_words;
+        w->span_bounds = k[W_SQUERIES]; w->span_events = k[W_SPAN];
+        // algorithmic bytes (DESIGN.md "Roofline"): locus in + result out, two bucket words per
+        // search pair, the search entries, per stop search the chunk words scanned, the word
+        // before the break chunk and its 8 CIGAR words; then per variant --
+        //   span:  the two span bounds of a query and its 16-B events;
+        //   event: rec + rec2 of every yielded read and rec of every overlap-failing one in
+        //          range, list offsets and list entries past the inline one
+        const uint64_t common = 24ull * n + 32ull * w->queries + 4ull * w->probe_entries +
+                                36ull * w->stop_searches + 4ull * w->stop_chunk_words;
+        if (c->gather == G_SPAN)
+            w->event_bytes = common + 16ull * w->span_bounds + 16ull * w->span_events;
+        else if (c->gather == G_EVENT)
+            w->event_bytes = common + 32ull * w->reads + 16ull * (w->range_reads - std::min(w->range_reads, w->reads)) +
+                             8ull * w->list_reads + 8ull * w->list_entries;
+        else
+            w->event_bytes = 24ull * n + 12ull * w->reads + 4ull * w->ops_walked;   // the variants walk CIGARs
     }
     return SVT_OK;
 }
@@ -2467,7 +2713,8 @@ static svt_status sw_1(svt_ctx *c, const svt_sw_query *q, size_t n, int32_t wind
             a.sw_sub = d_sub;
             a.sw_out = d_res;
             const dim3 grid((unsigned)((ns + WPB - 1) / WPB)), block(64 * WPB);
-            if (c->gather == G_EVENT) hipLaunchKernelGGL(sw_kernel<G_EVENT>, grid, block, 0, nullptr, a);
+            if (c->gather == G_SPAN) hipLaunchKernelGGL(sw_kernel<G_SPAN>, grid, block, 0, nullptr, a);
+            else if (c->gather == G_EVENT) hipLaunchKernelGGL(sw_kernel<G_EVENT>, grid, block, 0, nullptr, a);
             else if (c->gather == G_INDEX) hipLaunchKernelGGL(sw_kernel<G_INDEX>, grid, block, 0, nullptr, a);
             else if (c->gather == G_STREAM) hipLaunchKernelGGL(sw_kernel<G_STREAM>, grid, block, 0, nullptr, a);
             else hipLaunchKernelGGL(sw_kernel<G_PERREAD>, grid, block, 0, nullptr, a);

@@ -28,9 +28,9 @@ def engine_factory():
 
     engines = []
 
-    def make(params=None, gather="event"):
-        """gather: "event" (candidate-op lists, default), "index" (chunk-index walk), "stream" (full CIGAR stream) or
-        "perread" (per-read walk) -- the SVTREK_GATHER variants of the engine."""
+    def make(params=None, gather="span"):
+        """gather: "span" (span events, default), "event" (candidate-op lists), "index" (chunk-index walk),
+        "stream" (full CIGAR stream) or "perread" (per-read walk) -- the SVTREK_GATHER variants of the engine."""
         old = os.environ.get("SVTREK_GATHER")
         os.environ["SVTREK_GATHER"] = gather
         try:

@@ -98,11 +98,32 @@ def test_entry_points_restore_current_device(engine_factory):
     assert torch.cuda.current_device() == before
 
 
+def test_span_walk_counters(engine_factory):
+    """svt_work's span-walk counters (the default gather): event_bytes = their sum at the
+    documented sizes, the reference work equals the oracle's."""
+    r = _workload(n_loci=4000, seed=65)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    w = eng.count_work(r.loci)
+    n = len(r.loci)
+    _, ow = O.refine_batch(r.pileup, r.loci, threads=8, with_work=True)
+    assert (w["windows"], w["reads"], w["ops_walked"], w["candidates"]) == \
+        (ow["windows"], ow["reads"], ow["ops_walked"], ow["candidates"])
+    assert 0 < w["span_bounds"] <= w["queries"] <= w["windows"]
+    assert w["span_events"] >= w["candidates"] * 0.5
+    assert w["range_reads"] == 0 and w["list_entries"] == 0
+    exp = (24 * n + 32 * w["queries"] + 4 * w["probe_entries"] + 36 * w["stop_searches"]
+           + 4 * w["stop_chunk_words"] + 16 * w["span_bounds"] + 16 * w["span_events"])
+    assert w["event_bytes"] == exp
+    assert w["event_bytes"] < 24 * n + 12 * w["reads"] + 4 * w["ops_walked"]
+    _same(eng.refine(r.loci), O.refine_batch(r.pileup, r.loci, threads=8))
+
+
 def test_event_walk_counters(engine_factory):
     """svt_work's event-walk counters: internally consistent and event_bytes = their sum at
     the documented sizes; the counting launch's results equal the plain launch's."""
     r = _workload(n_loci=4000, seed=64)
-    eng = engine_factory()
+    eng = engine_factory(gather="event")
     eng.load_pileup(r.pileup)
     w = eng.count_work(r.loci)
     n = len(r.loci)

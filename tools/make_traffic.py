@@ -3,7 +3,7 @@
     python tools/make_traffic.py gpurun_out/prof_TAG profiles/TAG [--workload W] [--kernel K]
 
 Copies the kernel stats / PMC CSVs and bench logs into profiles/TAG and writes
-profiles/traffic.json for the timed kernel (default refine_event_kernel): HBM bytes per launch =
+profiles/traffic.json for the timed kernel (default refine_span_kernel): HBM bytes per launch =
 read bytes from the L2 fabric read requests by size class (TCC_EA0_RDREQ_{32B,64B,128B}:
 32/64/128 B each; cross-checked against 2 x FETCH_SIZE, which gfx950 tallies at 64 B per
 128-B request, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, median over the profiled
@@ -37,7 +37,7 @@ def main() -> int:
     ap.add_argument("src")
     ap.add_argument("dst")
     ap.add_argument("--workload", default="cfg4_1m_delins_30x_hifi")
-    ap.add_argument("--kernel", default="refine_event_kernel")
+    ap.add_argument("--kernel", default="refine_span_kernel")
     a = ap.parse_args()
     os.makedirs(a.dst, exist_ok=True)
     copies = {"trace/run_kernel_stats.csv": "kernel_stats.csv", "pmc_fetch/run_counter_collection.csv":
