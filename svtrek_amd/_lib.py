@@ -122,6 +122,15 @@ def load_engine() -> C.CDLL:
     path = engine_path()
     if not os.path.exists(path):
         raise RuntimeError(f"svtrek_amd HIP engine not built: {path} (run __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 and the
+    # engine's dependency on that soname binds to whichever copy is loaded first.  When the
+    # engine comes first, a later torch (device buffers, streams, RCCL) runs on the system
+    # copy and finds no GPUs, so torch -- where installed -- is loaded before the engine.
+    if os.environ.get("SVTREK_NO_TORCH_FIRST") is None:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = C.CDLL(path)
     P = C.c_void_p
     lib.svt_open.argtypes = [C.POINTER(SvtParams), C.c_int, C.POINTER(P)]

@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.9.0 (gfx950, span walk)"
+#define SVT_VERSION "svtrek_amd 0.9.1 (gfx950, span walk, band vote)"
 
 namespace {
 
@@ -1173,6 +1173,9 @@ __device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
     if (!read_range(P, tid, beg, end, lo, hi)) return;
+#if SVT_DIAG == 1
+    if (lo < hi) return;     // diagnostic build: region query only
+#endif
     const int ln = lane_id();
     const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
     const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
@@ -1209,7 +1212,7 @@ __device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_
             const int32_t idx = cnt + (int32_t)mbcnt(m);
             if (c && idx < sink.cap) sink.buf[idx] = (int32_t)val;
             cnt += (int32_t)__popcll(m);
-            if (KIND == K_END) {
+            if (KIND == K_END && SVT_DIAG != 3) {
                 uint64_t sm = ballot(brk);
                 if (sm) {   // the position after the break op, rare: the sink's LDS counter takes over
                     if (ln == 0) *sink.cnt = cnt;
@@ -1371,10 +1374,69 @@ __device__ __forceinline__ int32_t mean_cluster(int64_t tot, int32_t cnt, int32_
     return mean_round(tot, cnt);
 }
 
+// Band filter (exact): consensus_pos only ever reads elements within `range` of pos and
+// their clusters (within ci of them), i.e. values in (pos - range - ci, pos + range + ci),
+// plus three facts about the whole multiset: whether any element is <= pos+25 (where the
+// left pass starts, lower_bound), its minimum (upper_bound's A[0] < pos-25 test and the
+// right pass's first element) and its maximum (the right pass's start when that test
+// fails).  Both passes stop at the first out-of-range element, and every element between
+// the band and the pass start is out of range, so voting over the band's sorted elements
+// with those three facts visits the same elements with the same clusters.  Requires
+// range > 25 (the left start pos+25 is then inside the band) and |pos|, |values| < 2^30
+// (the reference's int32 differences cannot wrap); otherwise the full multiset is voted.
+struct Band {
+    bool on = false;
+    int32_t u = 0, gmin = 0, gmax = 0;   // #elements <= pos+25, min, max of the full multiset
+    int64_t lo = 0, hi = 0;              // open interval (lo, hi)
+    __device__ __forceinline__ bool in(int32_t x) const { return lo < (int64_t)x && (int64_t)x < hi; }
+};
+
+#ifndef SVT_BAND
+#define SVT_BAND 1
+#endif
+// Compacts buf[0..n) (n <= 4*WAVE) to its band elements in place; returns their count.
+__device__ __forceinline__ int32_t band_filter(int32_t *buf, int32_t n, int32_t pos, const KParams &k, Band &bd) {
+    const int ln = lane_id();
+    constexpr int E = 4;
+    int32_t x[E];
+    int32_t mn = INT32_MAX, mx = INT32_MIN, u = 0;
+#pragma unroll
+    for (int q = 0; q < E; q++) {
+        const int i = q * WAVE + ln;
+        x[q] = i < n ? buf[i] : 0;
+        if (i < n) { mn = min(mn, x[q]); mx = max(mx, x[q]); }
+        u += __popcll(ballot(i < n && x[q] <= pos + SV_MIN_LENGTH / 2));
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        mn = min(mn, __shfl_xor(mn, d, WAVE));
+        mx = max(mx, __shfl_xor(mx, d, WAVE));
+    }
+    constexpr int32_t LIM = 1 << 30;
+    if (k.range <= SV_MIN_LENGTH / 2 || pos <= -LIM || pos >= LIM || mn <= -LIM || mx >= LIM) return n;
+    const int64_t w = (int64_t)k.range + (int64_t)max(k.ci, 0);
+    bd.on = true;
+    bd.u = u; bd.gmin = mn; bd.gmax = mx;
+    bd.lo = (int64_t)pos - w;
+    bd.hi = (int64_t)pos + w;
+    wave_sync();
+    int32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < E; q++) {
+        const int i = q * WAVE + ln;
+        const bool keep = i < n && bd.in(x[q]);
+        const uint64_t m = ballot(keep);
+        if (keep) buf[cnt + (int32_t)mbcnt(m)] = x[q];
+        cnt += (int32_t)__popcll(m);
+    }
+    wave_sync();
+    return cnt;
+}
+
 // consensus_pos (refinement.c:41-101) on sorted A[0..n) with prefix sums P[0..n].
 // reg: x0 holds A[lane] for lanes < min(n, 64) (the register sorts), read instead of LDS.
 __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t pos, const KParams &k,
-                                        int32_t x0, bool reg) {
+                                        int32_t x0, bool reg, const Band &bd) {
     const int ln = lane_id();
     const int32_t ci = k.ci, range = k.range;
     int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
@@ -1387,6 +1449,10 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
         u += __popcll(ballot(i < n && (reg && b == 0 ? x0 : A[i]) <= pos + SV_MIN_LENGTH / 2));
     }
     int32_t p = u == 0 ? 0 : u - 1;
+    if (bd.on) {   // A = the band of the full multiset (see Band): start where the full pass would
+        p = bd.u == 0 ? 0 : u == 0 ? -1 : u - 1;   // u >= 1 elements <= pos+25 but none in the band:
+        if (n == 0) p = -1;                         // the full pass stops at once (below the band)
+    }
 
     // left pass: i = p, p-1, ... while |pos - A[i]| < range   (refinement.c:58-77)
     for (int32_t top = p; top >= 0; top -= WAVE) {
@@ -1416,6 +1482,8 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
 
     // upper_bound(A, n, pos-25): 0 if A[0] < pos-25 else n-1   (refinement.c:12-19)
     int32_t q = (n > 0 && (reg ? rdlane_i(x0, 0) : A[0]) < pos - SV_MIN_LENGTH / 2) ? 0 : n - 1;
+    if (bd.on)   // the full multiset's A[0] / A[n-1]: in the band they are A's first / last element
+        q = bd.gmin < pos - SV_MIN_LENGTH / 2 ? (bd.in(bd.gmin) ? 0 : n) : (bd.in(bd.gmax) ? n - 1 : n);
     for (int32_t bot = q; bot < n; bot += WAVE) {
         int32_t i = bot + ln;
         const int32_t ai = reg && bot == 0 ? x0 : A[i < n ? i : 0];
@@ -1483,6 +1551,8 @@ template <int VOTE>
 __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
                                                  int32_t &support) {
     const int ln = lane_id();
+    Band bd;
+    if (VOTE == V_CONSENSUS && SVT_BAND && n <= 4 * WAVE) n = band_filter(buf, n, pos, k, bd);
     int32_t x0 = 0;   // sorted element ln, from the register sorts (no LDS read-back below)
     if (n <= 16) x0 = reg_bitonic_sort<1, 16>(buf, n);
     else if (n <= 32) x0 = reg_bitonic_sort<1, 32>(buf, n);
@@ -1508,7 +1578,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
     wave_sync();
     if (SVT_DIAG == 5) return n;   // diagnostic build: sort + prefix sums, no vote
     if (VOTE == V_SLIDING) return sw_vote(buf, P, n, k, support);
-    return vote(buf, P, n, pos, k, x0, n <= 4 * WAVE);
+    return vote(buf, P, n, pos, k, x0, n <= 4 * WAVE, bd);
 }
 
 struct WinLds {

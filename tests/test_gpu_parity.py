@@ -323,3 +323,47 @@ def test_register_sort_sizes(engine_factory, ncand):
     got = eng.refine(loci)
     want = O.refine_batch(pl, loci, eng.params)
     _assert_same(got, want, loci)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_vote_band_edges(engine_factory, seed):
+    """The vote's band filter (svt_engine.hip band_filter) against the full-multiset oracle:
+    candidates exactly at / next to pos +- (range + ci), at pos+25 +- 1, far-left and far-right
+    noise (the upper_bound A[0] and the max), clusters straddling the band edge, and parameter
+    sets where the band is off (range <= 25, negative ci)."""
+    rng = np.random.default_rng(7000 + seed)
+    rows, vals = [], []
+    ci = int(rng.choice([-3, 0, 1, 5, 12]))
+    rng_ = int(rng.choice([10, 25, 26, 60, 500]))
+    mc = int(rng.choice([1, 2, 3, 4]))
+    eng = engine_factory(Params(consensus_interval=ci, consensus_interval_range=rng_, consensus_min_count=mc))
+    base = 300000
+    w = rng_ + max(ci, 0)
+    for k in range(60):
+        c = base + k * 60000
+        pos = c + int(rng.integers(-30, 30))
+        edge = [pos - w - 1, pos - w, pos - w + 1, pos + w - 1, pos + w, pos + w + 1,
+                pos + 24, pos + 25, pos + 26, pos - 24, pos - 25, pos - 26,
+                pos - rng_, pos - rng_ + 1, pos + rng_ - 1, pos + rng_]
+        v = []
+        for _ in range(int(rng.integers(0, 30))):
+            r = rng.random()
+            if r < 0.4:
+                v.append(int(rng.choice(edge)) + int(rng.integers(-1, 2)))
+            elif r < 0.6:
+                v.append(pos + int(rng.integers(-15000, -w)))     # far left noise (A[0])
+            elif r < 0.7:
+                v.append(pos + int(rng.integers(w, 1900)))        # far right noise (the max)
+            else:
+                v.append(pos + int(rng.integers(-w - 10, w + 10)))
+        if rng.random() < 0.3:   # a tight cluster straddling an edge
+            e0 = int(rng.choice(edge))
+            v.extend([e0 + int(d) for d in rng.integers(-abs(ci) - 2, abs(ci) + 3, size=int(rng.integers(2, 8)))])
+        vals.extend(v)
+        rows.append((2, 1, pos, c + 20000))
+    pl = cluster_pileup(vals)
+    eng.load_pileup(pl)
+    loci = make_loci(rows)
+    got = eng.refine(loci)
+    want = O.refine_batch(pl, loci, eng.params)
+    _assert_same(got, want, loci)

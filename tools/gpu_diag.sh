@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT=gpurun_out/diag_$TAG
 mkdir -p "$OUT"
 i=0
-for lib in svtrek_amd/libsvtrek_hip.so svtrek_amd/variants/*.so; do
+for lib in svtrek_amd/libsvtrek_hip.so svtrek_amd/diag/*.so; do
   name=$(basename "$lib" .so)
   for args in "$@"; do
     i=$((i+1))
