@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.9.1 (gfx950, span walk, band vote)"
+#define SVT_VERSION "svtrek_amd 0.9.4 (gfx950, span walk, band vote)"
 
 namespace {
 
@@ -126,7 +126,27 @@ constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status,
 static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
 
 // ------------------------------------------------------------------ wave primitives
-__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+#ifndef SVT_COLD_NOINLINE
+#define SVT_COLD_NOINLINE 0
+#endif
+#if SVT_COLD_NOINLINE
+#define SVT_COLD __noinline__
+#else
+#define SVT_COLD __forceinline__
+#endif
+#ifndef SVT_OPAQUE_LANE
+#define SVT_OPAQUE_LANE 0
+#endif
+// The lane id behind an empty volatile asm: lane-dependent values (the sort networks'
+// exchange masks, ...) are then recomputed where used instead of being hoisted out of the
+// batched kernel's per-window loop and held live across it (VGPR/SGPR pressure).
+__device__ __forceinline__ int lane_id() {
+    int l = (int)__lane_id();
+#if SVT_OPAQUE_LANE
+    asm volatile("" : "+v"(l));
+#endif
+    return l;
+}
 __device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ __forceinline__ int32_t rdlane_i(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -204,7 +224,7 @@ __device__ __forceinline__ int64_t wave_scan_add64(int64_t x) {
 
 // First index in [l, h) whose key satisfies pred (pred monotone false..true), 64-ary.
 template <typename Pred>
-__device__ __forceinline__ int64_t wave_partition_point(int64_t l, int64_t h, Pred pred) {
+__device__ SVT_COLD int64_t wave_partition_point(int64_t l, int64_t h, Pred pred) {   // cold: > 64 reads per bucket
     const int ln = lane_id();
     while (h - l > WAVE) {
         int64_t span = h - l;
@@ -1159,33 +1179,21 @@ __device__ __forceinline__ void span_count(const DevPileup &P, int tid, uint32_t
     }
 }
 
-template <int KIND, bool COUNT>
-__device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
-                                            WinStats &st) {
-    if (COUNT) {   // diagnostic: the reference's work by the exact per-read walk + what the span walk reads
-        gather_perread<KIND, true>(P, tid, s, e, sink, st);
-        if (e < 0x80000000u) span_count<KIND>(P, tid, s, e, st);
-        return;
-    }
-    // Event positions are walk positions < 2^29 (longer walks are flagged slow at load time
-    // and carry no events); windows ending at or past 2^31 take the exact per-read path.
-    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
-    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
-    int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi)) return;
-#if SVT_DIAG == 1
-    if (lo < hi) return;     // diagnostic build: region query only
-#endif
+// The span walk proper: events [E0, E1) of the yielded reads [lo, hi) of window [s, e]
+// (query beg = s-1), nslow = the slow reads among them.  Leaves the candidate count in
+// *sink.cnt.
+template <int KIND>
+__device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t s, uint32_t e, int64_t lo, int64_t hi,
+                                          uint64_t E0, uint64_t E1, uint64_t nslow, Sink &sink) {
+    const int64_t beg = (int64_t)(uint32_t)(s - 1u);
+    const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);   // read_range yielded reads: beg < end <= 2^31 - 1
     const int ln = lane_id();
-    const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
     const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
-    // one step: the span bounds (lanes 0, 1) and the slow-read count of [lo, hi) (lanes 2, 3)
-    const uint64_t ob = ln < 2 ? off[ln ? hi : lo] : ln < 4 ? P.slowpre[ln == 3 ? hi : lo] : 0ull;
     const uint64_t cbase = KIND == K_END ? P.off64[P.tid_off[tid]] : 0ull;   // stop searches' arena base
-    const uint64_t E0 = rdlane64(ob, 0), E1 = rdlane64(ob, 1), nslow = rdlane64(ob, 3) - rdlane64(ob, 2);
     int32_t cnt = 0;   // candidates appended so far (wave-uniform)
     for (uint64_t b = E0; b < E1; b += SPAN_U * WAVE) {
         uint4 v[SPAN_U];
+        const uint64_t left = E1 - b;   // events from b on (wave-uniform): the u-slots past them are skipped
 #pragma unroll
         for (int u = 0; u < SPAN_U; u++) {
             const uint64_t j = b + (uint64_t)(u * WAVE + ln);
@@ -1193,8 +1201,9 @@ __device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_
         }
 #pragma unroll
         for (int u = 0; u < SPAN_U; u++) {
+            if ((uint64_t)(u * WAVE) >= left) break;
             const uint32_t x = v[u].x, op = v[u].y & 0xfu, len = v[u].y >> 4;
-            const bool ovl = (int64_t)(int32_t)v[u].z > beg;   // hts_itr_next overlap; pos < end holds below hi
+            const bool ovl = (int32_t)v[u].z > beg32;   // hts_itr_next overlap; pos < end holds below hi
             bool c, brk = false;
             uint32_t val = x;
             if (KIND == K_INS) {
@@ -1226,6 +1235,7 @@ __device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_
     }
     if (ln == 0) *sink.cnt = cnt;
     if (nslow) {   // reads whose walk could leave the event range: exact per-read replay (never in practice)
+        WinStats st;
         wave_sync();
         for (int64_t rb = lo; rb < hi; rb += WAVE) {
             const int64_t r = rb + ln;
@@ -1239,6 +1249,31 @@ __device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_
             }
         }
     }
+}
+
+template <int KIND, bool COUNT>
+__device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
+                                            WinStats &st) {
+    if (COUNT) {   // diagnostic: the reference's work by the exact per-read walk + what the span walk reads
+        gather_perread<KIND, true>(P, tid, s, e, sink, st);
+        if (e < 0x80000000u) span_count<KIND>(P, tid, s, e, st);
+        return;
+    }
+    // Event positions are walk positions < 2^29 (longer walks are flagged slow at load time
+    // and carry no events); windows ending at or past 2^31 take the exact per-read path.
+    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
+    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
+    int64_t lo, hi;
+    if (!read_range(P, tid, beg, end, lo, hi)) return;
+#if SVT_DIAG == 1
+    if (lo < hi) return;     // diagnostic build: region query only
+#endif
+    const int ln = lane_id();
+    const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
+    // one step: the span bounds (lanes 0, 1) and the slow-read count of [lo, hi) (lanes 2, 3)
+    const uint64_t ob = ln < 2 ? off[ln ? hi : lo] : ln < 4 ? P.slowpre[ln == 3 ? hi : lo] : 0ull;
+    const uint64_t E0 = rdlane64(ob, 0), E1 = rdlane64(ob, 1), nslow = rdlane64(ob, 3) - rdlane64(ob, 2);
+    span_walk<KIND>(P, tid, s, e, lo, hi, E0, E1, nslow, sink);
 }
 
 // ------------------------------------------------------------------ sort + vote (A8-A10)
@@ -1354,7 +1389,7 @@ __device__ __forceinline__ int32_t first_geq(const int32_t *buf, int32_t l, int3
     return l;
 }
 
-__device__ __forceinline__ int32_t mean_round(int64_t tot, int32_t cnt) {
+__device__ SVT_COLD int32_t mean_round(int64_t tot, int32_t cnt) {   // cold: the 64-bit division
     // (int)((uint64 total + count/2) / count), refinement.c:66
     uint64_t t = (uint64_t)tot + (uint64_t)(int64_t)(cnt / 2);
     return (int32_t)(uint32_t)(t / (uint64_t)(int64_t)cnt);
@@ -1385,46 +1420,60 @@ __device__ __forceinline__ int32_t mean_cluster(int64_t tot, int32_t cnt, int32_
 // range > 25 (the left start pos+25 is then inside the band) and |pos|, |values| < 2^30
 // (the reference's int32 differences cannot wrap); otherwise the full multiset is voted.
 struct Band {
-    bool on = false;
-    int32_t u = 0, gmin = 0, gmax = 0;   // #elements <= pos+25, min, max of the full multiset
-    int64_t lo = 0, hi = 0;              // open interval (lo, hi)
-    __device__ __forceinline__ bool in(int32_t x) const { return lo < (int64_t)x && (int64_t)x < hi; }
+    bool on = false;    // the vote runs over the band's elements (else over the full multiset)
+    bool f32 = false;   // ... and every band element is >= 0: 32-bit cluster sums (vote<true>)
+    int32_t u = 0;      // #elements <= pos+25 of the full multiset (the left pass start)
+    int32_t n_lt = 0;   // #elements <  pos-25 (upper_bound's A[0] < pos-25 test)
+    int32_t n_le = 0;   // #elements <= lo (is the full minimum inside the band?)
+    int32_t n_ge = 0;   // #elements >= hi (is the full maximum inside the band?)
+    int32_t lo = 0, hi = 0;   // the band: open interval (lo, hi)
 };
 
 #ifndef SVT_BAND
 #define SVT_BAND 1
 #endif
 // Compacts buf[0..n) (n <= 4*WAVE) to its band elements in place; returns their count.
+// Counts only (ballots), no reductions; int32 compares throughout, since the band is only
+// used when |pos| < 2^30 and range + max(ci, 0) <= 2^22 (so lo, hi fit) and every element
+// is within +-2^30.
 __device__ __forceinline__ int32_t band_filter(int32_t *buf, int32_t n, int32_t pos, const KParams &k, Band &bd) {
+    constexpr int32_t LIM = 1 << 30, WMAX = 1 << 22;
+    if (k.range <= SV_MIN_LENGTH / 2 || pos <= -LIM || pos >= LIM || k.range > WMAX || k.ci > WMAX - k.range ||
+        k.ci < -WMAX)
+        return n;
     const int ln = lane_id();
+    const int32_t w = k.range + max(k.ci, 0);
+    const int32_t lo = pos - w, hi = pos + w;
     constexpr int E = 4;
     int32_t x[E];
-    int32_t mn = INT32_MAX, mx = INT32_MIN, u = 0;
+    int32_t u = 0, nlt = 0, nle = 0, nge = 0;
+    uint64_t bad = 0, neg = 0;
 #pragma unroll
     for (int q = 0; q < E; q++) {
+        x[q] = 0;
+        if (q * WAVE >= n) break;   // wave-uniform: blocks past n hold nothing
         const int i = q * WAVE + ln;
-        x[q] = i < n ? buf[i] : 0;
-        if (i < n) { mn = min(mn, x[q]); mx = max(mx, x[q]); }
-        u += __popcll(ballot(i < n && x[q] <= pos + SV_MIN_LENGTH / 2));
+        const bool v = i < n;
+        x[q] = v ? buf[i] : 0;
+        u += __popcll(ballot(v && x[q] <= pos + SV_MIN_LENGTH / 2));
+        nlt += __popcll(ballot(v && x[q] < pos - SV_MIN_LENGTH / 2));
+        nle += __popcll(ballot(v && x[q] <= lo));
+        nge += __popcll(ballot(v && x[q] >= hi));
+        bad |= ballot(v && (x[q] <= -LIM || x[q] >= LIM));
+        neg |= ballot(v && lo < x[q] && x[q] < hi && x[q] < 0);
     }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        mn = min(mn, __shfl_xor(mn, d, WAVE));
-        mx = max(mx, __shfl_xor(mx, d, WAVE));
-    }
-    constexpr int32_t LIM = 1 << 30;
-    if (k.range <= SV_MIN_LENGTH / 2 || pos <= -LIM || pos >= LIM || mn <= -LIM || mx >= LIM) return n;
-    const int64_t w = (int64_t)k.range + (int64_t)max(k.ci, 0);
+    if (bad) return n;
     bd.on = true;
-    bd.u = u; bd.gmin = mn; bd.gmax = mx;
-    bd.lo = (int64_t)pos - w;
-    bd.hi = (int64_t)pos + w;
+    bd.f32 = neg == 0;
+    bd.u = u; bd.n_lt = nlt; bd.n_le = nle; bd.n_ge = nge;
+    bd.lo = lo; bd.hi = hi;
     wave_sync();
     int32_t cnt = 0;
 #pragma unroll
     for (int q = 0; q < E; q++) {
+        if (q * WAVE >= n) break;
         const int i = q * WAVE + ln;
-        const bool keep = i < n && bd.in(x[q]);
+        const bool keep = i < n && lo < x[q] && x[q] < hi;
         const uint64_t m = ballot(keep);
         if (keep) buf[cnt + (int32_t)mbcnt(m)] = x[q];
         cnt += (int32_t)__popcll(m);
@@ -1433,10 +1482,31 @@ __device__ __forceinline__ int32_t band_filter(int32_t *buf, int32_t n, int32_t 
     return cnt;
 }
 
+__device__ __forceinline__ int32_t first_greater32(const int32_t *buf, int32_t l, int32_t h, int32_t key) {
+    while (l < h) {
+        int32_t m = (l + h) >> 1;
+        if (buf[m] > key) h = m; else l = m + 1;
+    }
+    return l;
+}
+__device__ __forceinline__ int32_t first_geq32(const int32_t *buf, int32_t l, int32_t h, int32_t key) {
+    while (l < h) {
+        int32_t m = (l + h) >> 1;
+        if (buf[m] >= key) h = m; else l = m + 1;
+    }
+    return l;
+}
+
 // consensus_pos (refinement.c:41-101) on sorted A[0..n) with prefix sums P[0..n].
 // reg: x0 holds A[lane] for lanes < min(n, 64) (the register sorts), read instead of LDS.
-__device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int32_t n, int32_t pos, const KParams &k,
-                                        int32_t x0, bool reg, const Band &bd) {
+// F32: A is a band with every element >= 0 and P holds 32-bit sums of A[j] - A0 (A0 = A[0]):
+// the reference's rounded uint64 mean (sum + c/2) / c of a cluster of non-negative values is
+// then A0 + (its offset sum + c/2) / c exactly, in 32 bits (offset sums < 2^31, band_filter).
+template <bool F32>
+__device__ __forceinline__ int32_t vote(const int32_t *A, const void *Pv, int32_t n, int32_t pos, const KParams &k,
+                                        int32_t x0, bool reg, const Band &bd, int32_t A0) {
+    const int64_t *P = reinterpret_cast<const int64_t *>(Pv);
+    const uint32_t *P32 = reinterpret_cast<const uint32_t *>(Pv);
     const int ln = lane_id();
     const int32_t ci = k.ci, range = k.range;
     int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
@@ -1463,9 +1533,15 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
         int32_t cnt = 0, cand = 0;
         if (ln < lim) {
             int32_t a = A[i];
-            int32_t kk = first_geq(A, 0, i, (int64_t)a - ci);   // contiguous j<i with a <= A[j]+ci
-            cnt = i - kk + 1;
-            cand = mean_cluster(P[i + 1] - P[kk], cnt, A[kk]);
+            if (F32) {
+                const int32_t kk = first_geq32(A, 0, i, a - ci);   // contiguous j<i with a <= A[j]+ci
+                cnt = i - kk + 1;
+                cand = A0 + (int32_t)((P32[i + 1] - P32[kk] + (uint32_t)(cnt / 2)) / (uint32_t)cnt);
+            } else {
+                int32_t kk = first_geq(A, 0, i, (int64_t)a - ci);   // contiguous j<i with a <= A[j]+ci
+                cnt = i - kk + 1;
+                cand = mean_cluster(P[i + 1] - P[kk], cnt, A[kk]);
+            }
         }
         // the greedy accept in pass order, visiting only elements whose count beats maxL
         const int32_t dd = ref_abs(pos - cand);
@@ -1483,7 +1559,7 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
     // upper_bound(A, n, pos-25): 0 if A[0] < pos-25 else n-1   (refinement.c:12-19)
     int32_t q = (n > 0 && (reg ? rdlane_i(x0, 0) : A[0]) < pos - SV_MIN_LENGTH / 2) ? 0 : n - 1;
     if (bd.on)   // the full multiset's A[0] / A[n-1]: in the band they are A's first / last element
-        q = bd.gmin < pos - SV_MIN_LENGTH / 2 ? (bd.in(bd.gmin) ? 0 : n) : (bd.in(bd.gmax) ? n - 1 : n);
+        q = bd.n_lt > 0 ? (bd.n_le == 0 ? 0 : n) : (bd.n_ge == 0 ? n - 1 : n);
     for (int32_t bot = q; bot < n; bot += WAVE) {
         int32_t i = bot + ln;
         const int32_t ai = reg && bot == 0 ? x0 : A[i < n ? i : 0];
@@ -1493,9 +1569,15 @@ __device__ __forceinline__ int32_t vote(const int32_t *A, const int64_t *P, int3
         int32_t cnt = 0, cand = 0;
         if (ln < lim) {
             int32_t a = ai;
-            int32_t m = first_greater(A, i + 1, n, (int64_t)a + ci);   // contiguous j>i with A[j] <= a+ci
-            cnt = m - i;
-            cand = mean_cluster(P[m] - P[i], cnt, a);
+            if (F32) {
+                const int32_t m = first_greater32(A, i + 1, n, a + ci);   // contiguous j>i with A[j] <= a+ci
+                cnt = m - i;
+                cand = A0 + (int32_t)((P32[m] - P32[i] + (uint32_t)(cnt / 2)) / (uint32_t)cnt);
+            } else {
+                int32_t m = first_greater(A, i + 1, n, (int64_t)a + ci);   // contiguous j>i with A[j] <= a+ci
+                cnt = m - i;
+                cand = mean_cluster(P[m] - P[i], cnt, a);
+            }
         }
         const int32_t dd = ref_abs(pos - cand);
         for (int l = -1;;) {
@@ -1547,14 +1629,21 @@ __device__ __forceinline__ int32_t sw_vote(const int32_t *A, const int64_t *P, i
 constexpr int V_CONSENSUS = 0, V_SLIDING = 1;
 
 // Sort + prefix sums + vote over buf[0..n) with scratch for P (n+1 int64).
-template <int VOTE>
+// LARGE: n > 4*WAVE is known (the spill slab): only the global bitonic + the int64 vote.
+template <int VOTE, bool LARGE = false>
 __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
                                                  int32_t &support) {
     const int ln = lane_id();
     Band bd;
-    if (VOTE == V_CONSENSUS && SVT_BAND && n <= 4 * WAVE) n = band_filter(buf, n, pos, k, bd);
+    if (!LARGE && VOTE == V_CONSENSUS && SVT_BAND && n <= 4 * WAVE) n = band_filter(buf, n, pos, k, bd);
     int32_t x0 = 0;   // sorted element ln, from the register sorts (no LDS read-back below)
-    if (n <= 16) x0 = reg_bitonic_sort<1, 16>(buf, n);
+    if (LARGE) {
+        int N = 1;
+        while (N < n) N <<= 1;
+        for (int i = n + ln; i < N; i += WAVE) buf[i] = INT32_MAX;
+        wave_sync();
+        wave_bitonic_sort(buf, N);
+    } else if (n <= 16) x0 = reg_bitonic_sort<1, 16>(buf, n);
     else if (n <= 32) x0 = reg_bitonic_sort<1, 32>(buf, n);
     else if (n <= WAVE) x0 = reg_bitonic_sort<1>(buf, n);
     else if (n <= 2 * WAVE) x0 = reg_bitonic_sort<2>(buf, n);
@@ -1566,11 +1655,27 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
         wave_sync();
         wave_bitonic_sort(buf, N);
     }
+    if (!LARGE && VOTE == V_CONSENSUS && bd.on && bd.f32) {   // 32-bit offset sums (see vote<true>)
+        uint32_t *P32 = reinterpret_cast<uint32_t *>(P);
+        const int32_t A0 = n > 0 ? rdlane_i(x0, 0) : 0;
+        uint32_t carry = 0;
+        if (ln == 0) P32[0] = 0;
+        for (int32_t b = 0; b < n; b += WAVE) {
+            const int32_t i = b + ln;
+            const uint32_t x = i < n ? (uint32_t)((b == 0 ? x0 : buf[i]) - A0) : 0u;
+            const uint32_t sc = carry + wave_scan_add(x);
+            if (i < n) P32[i + 1] = sc;
+            carry = rdlane(sc, WAVE - 1);
+        }
+        wave_sync();
+        if (SVT_DIAG == 5) return n;
+        return vote<true>(buf, P32, n, pos, k, x0, true, bd, A0);
+    }
     int64_t carry = 0;
     if (ln == 0) P[0] = 0;
     for (int32_t b = 0; b < n; b += WAVE) {
         int32_t i = b + ln;
-        int64_t x = i < n ? (int64_t)(b == 0 && n <= 4 * WAVE ? x0 : buf[i]) : 0;
+        int64_t x = i < n ? (int64_t)(!LARGE && b == 0 && n <= 4 * WAVE ? x0 : buf[i]) : 0;
         int64_t s = carry + wave_scan_add64(x);
         if (i < n) P[i + 1] = s;
         carry = (int64_t)rdlane64((uint64_t)s, WAVE - 1);
@@ -1578,7 +1683,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
     wave_sync();
     if (SVT_DIAG == 5) return n;   // diagnostic build: sort + prefix sums, no vote
     if (VOTE == V_SLIDING) return sw_vote(buf, P, n, k, support);
-    return vote(buf, P, n, pos, k, x0, n <= 4 * WAVE, bd);
+    return vote<false>(buf, P, n, pos, k, x0, !LARGE && n <= 4 * WAVE, bd, 0);
 }
 
 struct WinLds {
@@ -1607,6 +1712,10 @@ __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, u
     return uniform_i(*sink.cnt);
 }
 
+template <int KIND, bool COUNT, int G, int VOTE>
+__device__ __forceinline__ int32_t vote_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e,
+                                               uint32_t imprecise, int32_t n, unsigned long long *wk, int32_t &support);
+
 template <int KIND, bool COUNT, int G, int VOTE = V_CONSENSUS>
 __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e, uint32_t imprecise,
                                  unsigned long long *wk, int32_t &support) {
@@ -1619,6 +1728,13 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
         wk[W_LENTRIES] += st.lentries; wk[W_STOPS] += st.stops; wk[W_STOPCH] += st.stopch;
         wk[W_SQUERIES] += st.squeries; wk[W_SPAN] += st.span;
     }
+    return vote_window<KIND, COUNT, G, VOTE>(a, lds, chrom, s, e, imprecise, n, wk, support);
+}
+
+// After the gather: n candidates in lds.cand (the first CAP of them) -> consensus_pos.
+template <int KIND, bool COUNT, int G, int VOTE>
+__device__ __forceinline__ int32_t vote_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e,
+                                               uint32_t imprecise, int32_t n, unsigned long long *wk, int32_t &support) {
     support = 0;
     if (n < a.prm.min_count) return -1;                    // refinement.c:43-45 (sliding: no support >= min_count)
     if (SVT_DIAG == 4) return n;   // diagnostic build: no sort/vote
@@ -1649,7 +1765,7 @@ __device__ __forceinline__ int32_t refine_window(const KArgs &a, WinLds &lds, in
     WinStats st2;
     Sink s2{g, N, &lds.ncand};
     gather<KIND, false, G>(a, chrom - 1, s, e, s2, st2, lds);
-    return sort_and_vote<VOTE>(g, gp, n, (int32_t)imprecise, a.prm, support);
+    return sort_and_vote<VOTE, true>(g, gp, n, (int32_t)imprecise, a.prm, support);
 }
 
 // One wave per query window, WPB independent waves per workgroup.  Window g < n is locus
@@ -1700,6 +1816,40 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_index_kernel(KArgs a)
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_event_kernel(KArgs a) { refine_body<false, G_EVENT>(a); }
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_span_kernel(KArgs a) { refine_body<false, G_SPAN>(a); }
 
+__device__ __forceinline__ void write_result(const KArgs &a, uint32_t li, uint32_t w, uint32_t r) {
+    if (a.rec_out) {   // gather record {index, start, end, 0}
+        uint32_t *o = reinterpret_cast<uint32_t *>(a.rec_out + li);
+        o[1 + w] = r;
+        if (w == 0) {
+            o[0] = a.rec_index ? a.rec_index[li] : a.rec_base + li;
+            o[3] = 0u;
+        }
+    } else {
+        uint32_t *o = reinterpret_cast<uint32_t *>(a.out + li);
+        o[w] = r;
+    }
+}
+
+// The gather of one window kind (+ the COUNT builds' work counters); the candidates are
+// left in lds.cand, their count is returned.
+template <int KIND, bool COUNT, int G>
+__device__ __forceinline__ int32_t gather_window(const KArgs &a, WinLds &lds, int chrom, uint32_t s, uint32_t e,
+                                                 unsigned long long *wk) {
+    WinStats st;
+    Sink sink{lds.cand, CAP, &lds.ncand};
+    const int32_t n = gather<KIND, COUNT, G>(a, chrom - 1, s, e, sink, st, lds);
+    if (COUNT && lane_id() == 0) {
+        wk[W_WINDOWS] += 1; wk[W_READS] += st.reads; wk[W_OPS] += st.ops; wk[W_CANDS] += (unsigned long long)n;
+        wk[W_QUERIES] += st.queries; wk[W_PROBE] += st.probe; wk[W_RANGE] += st.range; wk[W_LREADS] += st.lreads;
+        wk[W_LENTRIES] += st.lentries; wk[W_STOPS] += st.stops; wk[W_STOPCH] += st.stopch;
+        wk[W_SQUERIES] += st.squeries; wk[W_SPAN] += st.span;
+    }
+    return n;
+}
+
+#ifndef SVT_SHARED_VOTE
+#define SVT_SHARED_VOTE 1
+#endif
 template <bool COUNT, int G>
 __device__ __forceinline__ void refine_body(const KArgs &a) {
     __shared__ WinLds lds_all[WPB];
@@ -1716,37 +1866,44 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
     const int32_t type = uniform_i(L.type), chrom = uniform_i(L.chrom);
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
     unsigned long long wk[W_N] = {};
-    uint32_t r = SVT_NA;
-    int32_t sup;
     const KParams &k = a.prm;
-    if (type == T_INS) {                                   // audit.c:176-187
-        if (w == 0) {
-            uint32_t s = pos - (uint32_t)k.median, e = pos + (uint32_t)k.median;
-            r = (uint32_t)refine_window<K_INS, COUNT, G>(a, lds, chrom, s, e, pos, wk, sup);
-        }
-    } else if (type == T_DEL) {                            // audit.c:188-220
-        if (w == 0) {
-            uint32_t s = pos - (uint32_t)k.wider, e = pos + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_START, COUNT, G>(a, lds, chrom, s, e, pos, wk, sup);
-        } else {
-            uint32_t s = end - (uint32_t)k.narrow, e = end + (uint32_t)k.narrow;
-            r = (uint32_t)refine_window<K_END, COUNT, G>(a, lds, chrom, s, e, end, wk, sup);
-        }
+    // A2 (audit.c:176-225): the window of this wave.  INV: refine_point collects only when
+    // sv_type == SV_INS (refinement.c:250), so both windows vote on 0 candidates -> -1 for
+    // every min_count >= 1 (validated): NA, NA.
+    int kind = -1;
+    uint32_t s = 0, e = 0, imp = 0;
+    if (type == T_INS && w == 0) {
+        kind = K_INS; s = pos - (uint32_t)k.median; e = pos + (uint32_t)k.median; imp = pos;
+    } else if (type == T_DEL) {
+        if (w == 0) { kind = K_START; s = pos - (uint32_t)k.wider; e = pos + (uint32_t)k.narrow; imp = pos; }
+        else { kind = K_END; s = end - (uint32_t)k.narrow; e = end + (uint32_t)k.narrow; imp = end; }
     }
-    // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250), so both
-    // windows vote on 0 candidates -> -1 for every min_count >= 1 (validated): NA, NA.
+    uint32_t r = SVT_NA;
+#if !SVT_SHARED_VOTE
+    int32_t sup = 0;
+    if (kind == K_INS) r = (uint32_t)refine_window<K_INS, COUNT, G>(a, lds, chrom, s, e, imp, wk, sup);
+    else if (kind == K_START) r = (uint32_t)refine_window<K_START, COUNT, G>(a, lds, chrom, s, e, imp, wk, sup);
+    else if (kind == K_END) r = (uint32_t)refine_window<K_END, COUNT, G>(a, lds, chrom, s, e, imp, wk, sup);
+#else
+    if (kind >= 0) {
+        // the kind-specific gathers, then ONE copy of the sort + vote for all kinds (code size:
+        // the three inlined copies of the vote no longer compete for the instruction cache)
+        int32_t n;
+        if (kind == K_INS) n = gather_window<K_INS, COUNT, G>(a, lds, chrom, s, e, wk);
+        else if (kind == K_START) n = gather_window<K_START, COUNT, G>(a, lds, chrom, s, e, wk);
+        else n = gather_window<K_END, COUNT, G>(a, lds, chrom, s, e, wk);
+        n = uniform_i(n);
+        int32_t sup = 0;
+        if (n < k.min_count) r = SVT_NA;                    // refinement.c:43-45
+        else if (SVT_DIAG == 4) r = (uint32_t)n;           // diagnostic build: no sort/vote
+        else if (n <= CAP) r = (uint32_t)sort_and_vote<V_CONSENSUS>(lds.cand, lds.pre, n, (int32_t)imp, k, sup);
+        else if (kind == K_INS) r = (uint32_t)vote_window<K_INS, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
+        else if (kind == K_START) r = (uint32_t)vote_window<K_START, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
+        else r = (uint32_t)vote_window<K_END, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
+    }
+#endif
     if (lane_id() == 0) {
-        if (a.rec_out) {   // gather record {index, start, end, 0}
-            uint32_t *o = reinterpret_cast<uint32_t *>(a.rec_out + li);
-            o[1 + w] = r;
-            if (w == 0) {
-                o[0] = a.rec_index ? a.rec_index[li] : a.rec_base + li;
-                o[3] = 0u;
-            }
-        } else {
-            uint32_t *o = reinterpret_cast<uint32_t *>(a.out + li);
-            o[w] = r;
-        }
+        write_result(a, li, w, r);
         if (COUNT)
             for (int i = 0; i < W_N; i++)
                 if (wk[i]) atomicAdd(a.work + i, wk[i]);
