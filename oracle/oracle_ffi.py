@@ -50,6 +50,8 @@ def lib() -> C.CDLL:
         L.orc_refine_ins.restype = C.c_int
         L.orc_refine_batch.argtypes = [P, P, P, C.c_size_t, P, C.c_int, P]
         L.orc_refine_batch.restype = C.c_int
+        L.orc_bgzf_refine_batch.argtypes = [C.c_char_p, P, P, C.c_size_t, P, C.c_int, P, C.c_char_p, C.c_size_t]
+        L.orc_bgzf_refine_batch.restype = C.c_int
         L.orc_parse_line.argtypes = [C.c_char_p, P, C.c_char_p, C.c_size_t]
         L.orc_parse_line.restype = C.c_int
         L.orc_format_result.argtypes = [P, P, C.c_char_p, C.c_size_t]
@@ -97,6 +99,24 @@ def refine_batch(pl, loci: np.ndarray, prm=None, threads: int = 1, with_work: bo
     del keep
     if with_work:
         return out, {f: int(getattr(w, f)) for f, _ in OrcWork._fields_}
+    return out
+
+
+def bgzf_refine_batch(bam_path: str, loci: np.ndarray, prm=None, threads: int = 1, with_stats: bool = False):
+    """The reference-shaped baseline (bgzf_ref.c): per-thread BAM handle + BAI, per-query
+    linear-index seek, BGZF inflate and record decode.  Needs `bam_path`.bai."""
+    from svtrek_amd._lib import RESULT_DTYPE
+    pr = params(prm)
+    loci = np.ascontiguousarray(loci)
+    out = np.empty(len(loci), dtype=RESULT_DTYPE)
+    st = (C.c_uint64 * 3)()
+    err = C.create_string_buffer(512)
+    rc = lib().orc_bgzf_refine_batch(bam_path.encode(), C.byref(pr), loci.ctypes.data, len(loci), out.ctypes.data,
+                                     threads, st, err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode() or "orc_bgzf_refine_batch failed")
+    if with_stats:
+        return out, {"blocks_inflated": int(st[0]), "bytes_inflated": int(st[1]), "records_decoded": int(st[2])}
     return out
 
 

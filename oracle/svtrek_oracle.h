@@ -53,6 +53,24 @@ int orc_refine_point(const orc_pileup *p, int sv_type, int chrom, uint32_t s, ui
 int orc_refine_ins  (const orc_pileup *p, int chrom, uint32_t s, uint32_t e,
                      uint32_t imprecise_pos, const orc_params *prm, orc_work *w);
 
+/* A read source for one region query (A3): returns a pileup and the range [*lo, *hi) of
+ * its reads that holds every read yielded for (tid, [beg, end)) -- a superset is fine, the
+ * walk applies the yield test (pos < end && endpos > beg) itself; NULL = no reads. */
+typedef const orc_pileup *(*orc_fetch_fn)(void *ctx, int tid, int64_t beg, int64_t end, int64_t *lo, int64_t *hi);
+/* A2 + A4..A10 of one record with reads from `fetch` (the in-memory pileup, or
+ * bgzf_ref.c's per-query BGZF reader). */
+void orc_refine_locus_src(orc_fetch_fn fetch, void *ctx, const orc_params *prm, const orc_locus *l,
+                          orc_result *r, orc_work *w);
+
+/* The reference-shaped CPU baseline (bgzf_ref.c): `threads` workers, each
+ * with its own file handle and its own copy of the BAI (audit.c:269-272), every region query
+ * seeking to the BAI's linear-index offset and inflating + decoding the BGZF blocks from
+ * there (htslib's sam_itr_queryi/sam_itr_next with no block cache, refinement.c:114-117).
+ * Loci are handed out in VCF order.  0 on success; -1 on an I/O / format error (message in
+ * err).  stats (may be NULL): [0] blocks inflated, [1] bytes inflated, [2] records decoded. */
+int orc_bgzf_refine_batch(const char *bam_path, const orc_params *prm, const orc_locus *loci, size_t n,
+                          orc_result *out, int threads, uint64_t *stats, char *err, size_t errcap);
+
 /* A2 windows + A4..A7 for one parsed record (the deletion/insertion/inversion wrappers). */
 void orc_refine_locus(const orc_pileup *p, const orc_params *prm, const orc_locus *l,
                       orc_result *r, orc_work *w);

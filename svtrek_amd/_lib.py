@@ -197,6 +197,8 @@ def load_sim() -> C.CDLL:
         getattr(lib, name).restype = P
     lib.sim_write_bam.argtypes = [P, C.c_char_p, C.c_int, C.c_int]
     lib.sim_write_bam.restype = C.c_int
+    lib.sim_write_bam_region.argtypes = [P, C.c_char_p, C.c_int, C.c_int, C.c_int32, C.c_int64, C.c_int64, C.c_int]
+    lib.sim_write_bam_region.restype = C.c_int
     lib.sim_insseq.argtypes = [P, C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(P),
                                C.POINTER(P)]
     lib.sim_insseq.restype = C.c_int

@@ -92,7 +92,7 @@ def build_sim(force: bool = False) -> str:
 def build_oracle(force: bool = False) -> str:
     """Test infrastructure: the CPU parity oracle (oracle/Makefile)."""
     out = os.path.join(ROOT, "oracle", "liboracle.so")
-    src = [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "poa_oracle.c", "svtrek_oracle.h", "Makefile")]
+    src = [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "poa_oracle.c", "bgzf_ref.c", "svtrek_oracle.h", "Makefile")]
     if force or _stale(out, src):
         _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + (["-B"] if force else []))
     return out

@@ -463,7 +463,11 @@ typedef struct {
     size_t n;
     int level;
     int err;
+    uint64_t coff;   /* compressed bytes written so far = the current block's file offset */
 } bgzf_w;
+
+/* BGZF virtual offset of the next byte written (SAM spec 4.1.1). */
+static uint64_t bgzf_voff(const bgzf_w *w) { return w->coff << 16 | (uint64_t)w->n; }
 
 static void bgzf_flush(bgzf_w *w) {
     if (w->err) return;
@@ -487,6 +491,7 @@ static void bgzf_flush(bgzf_w *w) {
     uint32_t isz = (uint32_t)w->n;
     t[4] = isz & 0xff; t[5] = (isz >> 8) & 0xff; t[6] = (isz >> 16) & 0xff; t[7] = isz >> 24;
     if (fwrite(out, 1, bsize, w->f) != bsize) w->err = 1;
+    w->coff += bsize;
     w->n = 0;
 }
 static void bgzf_put(bgzf_w *w, const void *data, size_t len) {
@@ -512,9 +517,108 @@ static int reg2bin(int64_t beg, int64_t end) {
     return 0;
 }
 
+/* ---------------------------------------------------------------- BAI (SAM spec 5.2) */
+typedef struct { uint64_t beg, end; } bai_chunk;
+typedef struct { uint32_t bin; int32_t n, cap; bai_chunk *c; } bai_bin;
+typedef struct {
+    bai_bin *bins;        /* indexed by bin number (37450 per reference, allocated lazily) */
+    uint32_t *used;       /* bin numbers in first-use order */
+    int32_t n_used;
+    uint64_t *ioff;       /* linear index: 16 kb windows */
+    int32_t n_intv, cap_intv;
+} bai_ref;
+
+#define BAI_NBIN 37450
+
+static int bai_add(bai_ref *r, uint32_t bin, uint64_t beg, uint64_t end, int64_t pos, int64_t endpos) {
+    if (!r->bins) {
+        r->bins = (bai_bin *)calloc(BAI_NBIN, sizeof(bai_bin));
+        r->used = (uint32_t *)malloc(BAI_NBIN * sizeof(uint32_t));
+        if (!r->bins || !r->used) return -1;
+    }
+    bai_bin *b = &r->bins[bin];
+    if (b->n == 0 && b->cap == 0) r->used[r->n_used++] = bin;
+    b->bin = bin;
+    if (b->n && b->c[b->n - 1].end == beg) {
+        b->c[b->n - 1].end = end;   /* adjacent records of one bin: one chunk */
+    } else {
+        if (b->n == b->cap) {
+            int32_t nc = b->cap ? 2 * b->cap : 4;
+            bai_chunk *x = (bai_chunk *)realloc(b->c, (size_t)nc * sizeof(bai_chunk));
+            if (!x) return -1;
+            b->c = x; b->cap = nc;
+        }
+        b->c[b->n++] = (bai_chunk){beg, end};
+    }
+    /* linear index: every 16 kb window the record overlaps keeps its smallest offset */
+    int64_t w0 = pos >> 14, w1 = (endpos > pos ? endpos - 1 : pos) >> 14;
+    if (w1 >= r->cap_intv) {
+        int32_t nc = r->cap_intv ? r->cap_intv : 64;
+        while (nc <= w1) nc *= 2;
+        uint64_t *x = (uint64_t *)realloc(r->ioff, (size_t)nc * sizeof(uint64_t));
+        if (!x) return -1;
+        for (int32_t i = r->cap_intv; i < nc; i++) x[i] = UINT64_MAX;
+        r->ioff = x; r->cap_intv = nc;
+    }
+    for (int64_t k = w0; k <= w1; k++)
+        if (r->ioff[k] == UINT64_MAX) r->ioff[k] = beg;
+    if (w1 + 1 > r->n_intv) r->n_intv = (int32_t)(w1 + 1);
+    return 0;
+}
+
+static int bai_write(bai_ref *refs, int32_t n_ref, const char *path) {
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    int err = fwrite("BAI\1", 1, 4, f) != 4;
+    err |= fwrite(&n_ref, 4, 1, f) != 1;
+    for (int32_t t = 0; t < n_ref; t++) {
+        bai_ref *r = &refs[t];
+        err |= fwrite(&r->n_used, 4, 1, f) != 1;
+        for (int32_t i = 0; i < r->n_used; i++) {
+            bai_bin *b = &r->bins[r->used[i]];
+            err |= fwrite(&b->bin, 4, 1, f) != 1;
+            err |= fwrite(&b->n, 4, 1, f) != 1;
+            err |= fwrite(b->c, sizeof(bai_chunk), (size_t)b->n, f) != (size_t)b->n;
+        }
+        /* empty windows take the next non-empty window's offset (windows are monotone in a
+         * coordinate-sorted file, so a query starting in an empty window loses nothing) */
+        uint64_t nxt = 0;
+        for (int32_t k = r->n_intv - 1; k >= 0; k--) {
+            if (r->ioff[k] == UINT64_MAX) r->ioff[k] = nxt;
+            else nxt = r->ioff[k];
+        }
+        err |= fwrite(&r->n_intv, 4, 1, f) != 1;
+        if (r->n_intv) err |= fwrite(r->ioff, 8, (size_t)r->n_intv, f) != (size_t)r->n_intv;
+    }
+    uint64_t n_no_coor = 0;
+    err |= fwrite(&n_no_coor, 8, 1, f) != 1;
+    if (fclose(f)) err = 1;
+    return err ? -1 : 0;
+}
+
+static void bai_free(bai_ref *refs, int32_t n_ref) {
+    if (!refs) return;
+    for (int32_t t = 0; t < n_ref; t++) {
+        if (refs[t].bins)
+            for (int32_t i = 0; i < refs[t].n_used; i++) free(refs[t].bins[refs[t].used[i]].c);
+        free(refs[t].bins); free(refs[t].used); free(refs[t].ioff);
+    }
+    free(refs);
+}
+
 int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level) {
+    return sim_write_bam_region(p, path, with_seq, level, -1, 0, 0, 0);
+}
+
+int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, int level, int32_t rtid, int64_t rbeg,
+                         int64_t rend, int write_bai) {
     bgzf_w *w = (bgzf_w *)calloc(1, sizeof(bgzf_w));
     if (!w) return -1;
+    bai_ref *bai = NULL;
+    if (write_bai && !(bai = (bai_ref *)calloc((size_t)(p->n_targets > 0 ? p->n_targets : 1), sizeof(bai_ref)))) {
+        free(w);
+        return -1;
+    }
     w->f = fopen(path, "wb");
     if (!w->f) { free(w); return -1; }
     w->level = level < 0 ? 6 : level;
@@ -550,7 +654,9 @@ int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level
     size_t rec_cap = 0;
     static const char nt16[] = "=ACMGRSVTWYHKDBN";
     for (int t = 0; t < p->n_targets; t++) {
+        if (rtid >= 0 && t != rtid) continue;
         for (int64_t r = p->tid_off[t]; r < p->tid_off[t + 1]; r++) {
+            if (rtid >= 0 && !(p->pos[r] < rend && p->endpos[r] > rbeg)) continue;
             const uint32_t *ops = p->cigar + p->cig_off[r];
             uint64_t n = p->cig_off[r + 1] - p->cig_off[r];
             int64_t qlen = 0, rlen = 0;
@@ -603,7 +709,10 @@ int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level
             }
             int32_t bs = (int32_t)(q - rec - 4);
             memcpy(rec, &bs, 4);
+            const uint64_t vbeg = bgzf_voff(w);
             bgzf_put(w, rec, (size_t)(q - rec));
+            if (bai && bai_add(&bai[t], (uint32_t)reg2bin(p->pos[r], p->endpos[r]), vbeg, bgzf_voff(w), p->pos[r],
+                               p->endpos[r])) w->err = 1;
         }
     }
     free(rec);
@@ -613,5 +722,17 @@ int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level
     int err = w->err;
     if (fclose(w->f)) err = 1;
     free(w);
+    if (bai && !err) {
+        size_t L = strlen(path);
+        char *bp = (char *)malloc(L + 5);
+        if (!bp) err = 1;
+        else {
+            memcpy(bp, path, L);
+            memcpy(bp + L, ".bai", 5);
+            if (bai_write(bai, p->n_targets, bp)) err = 1;
+            free(bp);
+        }
+    }
+    bai_free(bai, p->n_targets);
     return err ? -1 : 0;
 }

@@ -73,6 +73,11 @@ void sim_free_buf(void *x);
 /* Write the pileup as a BGZF-compressed, coordinate-sorted BAM.  with_seq != 0 stores
  * random SEQ/QUAL of the CIGAR's query length (realistic ingest cost).  0 on success. */
 int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level);
+/* The same, restricted to the records of contig `tid` overlapping [beg, end) (tid < 0: all
+ * records), and with write_bai != 0 also `path`.bai: bins + chunks + the 16 kb linear index
+ * (SAM spec 5.2; empty windows hold the next window's offset).  0 on success. */
+int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, int level, int32_t tid, int64_t beg,
+                         int64_t end, int write_bai);
 
 #ifdef __cplusplus
 }

@@ -163,11 +163,17 @@ def insertion_sequences(res: SimResult, cfg: SimConfig, err_permille: int = 50) 
     return off, bases
 
 
-def write_bam(res: SimResult, path: str, with_seq: bool = False, level: int = 6) -> None:
+def write_bam(res: SimResult, path: str, with_seq: bool = False, level: int = 6, bai: bool = True,
+              region: tuple[int, int, int] | None = None) -> None:
+    """Coordinate-sorted BAM of the pileup (+ `path`.bai unless bai=False; the reference needs
+    one, audit.c:271).  region = (tid, beg, end): only the records of that contig overlapping
+    [beg, end) -- every query inside the region yields the same reads as on the full file."""
     if res.handle is None:
         raise ValueError("generate(..., keep_handle=True) is required to write a BAM")
     lib = load_sim()
-    if lib.sim_write_bam(res.handle.h, path.encode(), 1 if with_seq else 0, level) != 0:
+    t, b, e = region if region is not None else (-1, 0, 0)
+    if lib.sim_write_bam_region(res.handle.h, path.encode(), 1 if with_seq else 0, level, t, b, e,
+                                1 if bai else 0) != 0:
         raise OSError(f"sim_write_bam failed: {path}")
 
 
