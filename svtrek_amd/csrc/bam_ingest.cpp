@@ -77,6 +77,14 @@ struct BgzfReader {
     bool eof = false;
     std::string err;
 
+    // Continue at compressed file offset `coff` (a BGZF block start).
+    bool seek(uint64_t coff) {
+        comp.clear();
+        eof = false;
+        if (fseeko(f, (off_t)coff, SEEK_SET) != 0) { err = "cannot seek in BAM (BAI offset past the end?)"; return false; }
+        return true;
+    }
+
     // Append the next batch of inflated blocks to `out`; false at end of file / on error.
     bool next(std::vector<uint8_t> &out) {
         const size_t CHUNK = 64u << 20;
@@ -152,6 +160,48 @@ struct BgzfReader {
             comp.erase(comp.begin(), comp.begin() + (ptrdiff_t)p);
             return true;
         }
+    }
+};
+
+// The BAI's linear index (SAM spec 5.2): per contig, the smallest virtual offset of the
+// records overlapping each 16 kb window.  Bins are skipped: a coordinate-sorted file read
+// from the linear-index offset reaches every record a region query can yield.
+struct BaiLinear {
+    std::vector<std::vector<uint64_t>> ioff;
+    bool load(const std::string &path, std::string &err) {
+        FILE *f = fopen(path.c_str(), "rb");
+        if (!f) { err = "cannot open BAI: " + path; return false; }
+        auto rd = [&](void *p, size_t n) { return fread(p, 1, n, f) == n; };
+        char magic[4];
+        int32_t n_ref = 0;
+        bool ok = rd(magic, 4) && memcmp(magic, "BAI\1", 4) == 0 && rd(&n_ref, 4) && n_ref >= 0;
+        if (ok) ioff.resize((size_t)n_ref);
+        for (int32_t r = 0; ok && r < n_ref; r++) {
+            int32_t n_bin = 0;
+            ok = rd(&n_bin, 4) && n_bin >= 0;
+            for (int32_t i = 0; ok && i < n_bin; i++) {
+                uint32_t bin;
+                int32_t n_chunk;
+                ok = rd(&bin, 4) && rd(&n_chunk, 4) && n_chunk >= 0 && fseeko(f, 16 * (off_t)n_chunk, SEEK_CUR) == 0;
+            }
+            int32_t n_intv = 0;
+            ok = ok && rd(&n_intv, 4) && n_intv >= 0;
+            if (ok) {
+                ioff[(size_t)r].resize((size_t)n_intv);
+                ok = n_intv == 0 || rd(ioff[(size_t)r].data(), 8 * (size_t)n_intv);
+            }
+        }
+        fclose(f);
+        if (!ok) err = "corrupt BAI: " + path;
+        return ok;
+    }
+    // Where a read of the records from (tid, beg) on starts; false = no such record.
+    bool start(int32_t tid, int64_t beg, uint64_t &voff) const {
+        for (size_t t = (size_t)std::max(tid, 0); t < ioff.size(); t++) {
+            const int64_t w = (int32_t)t == tid ? std::max<int64_t>(beg, 0) >> 14 : 0;
+            if (w < (int64_t)ioff[t].size()) { voff = ioff[t][(size_t)w]; return true; }
+        }
+        return false;
     }
 };
 
@@ -298,6 +348,12 @@ struct svth_bam {
 extern "C" {
 
 svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap) {
+    return svth_bam_read_region(path, threads, -1, 0, -1, 0, err, errcap);
+}
+
+svth_bam *svth_bam_read_region(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
+                               char *err, size_t errcap) {
+    const bool region = tid0 >= 0;
     auto fail = [&](const std::string &m) -> svth_bam * {
         if (err && errcap) snprintf(err, errcap, "%s", m.c_str());
         return nullptr;
@@ -334,6 +390,23 @@ svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap)
         b->names.emplace_back((const char *)buf.data() + at + 4, ln ? ln - 1 : 0);
         at += 4 + ln + 4;
     }
+    // region: continue at the BAI's linear-index offset of (tid0, beg0)
+    bool done = false;
+    if (region) {
+        BaiLinear bai;
+        std::string e;
+        if (!bai.load(std::string(path) + ".bai", e)) return bail(e);
+        uint64_t voff = 0;
+        if (!bai.start(tid0, beg0, voff)) done = true;   // no record at or after the region start
+        else {
+            if (!rd.seek(voff >> 16)) return bail("cannot seek in BAM");
+            buf.clear();
+            at = 0;
+            const size_t uo = (size_t)(voff & 0xffff);
+            if (uo && !need(uo)) return bail("BAI offset past the end of the BAM");
+            at += uo;
+        }
+    }
     // records, chunk by chunk
     RawVec<int32_t> tid_of;
     std::vector<uint8_t> rec_ok;
@@ -342,7 +415,7 @@ svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap)
     std::vector<size_t> roff;
     std::vector<uint32_t> rlen;
     std::vector<RecView> views;
-    for (;;) {
+    while (!done) {
         if (buf.size() - at < 4 && !need(4)) break;   // clean EOF
         // sequential boundary scan over the complete records in the buffer
         roff.clear();
@@ -359,12 +432,22 @@ svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap)
             continue;
         }
         // pass 1 (parallel): locate every record's CIGAR
-        const size_t nr = roff.size();
+        size_t nr = roff.size();
         views.resize(nr);
         parallel_for(rd.threads, nr, [&](size_t i0, size_t i1) {
             for (size_t i = i0; i < i1; i++)
                 views[i] = view_record(buf.data() + roff[i], rd32(buf.data() + roff[i] - 4), n_ref);
         });
+        if (region)   // sorted file: the first record past (tid1, end1) ends the read
+            for (size_t i = 0; i < nr; i++) {
+                const int32_t t = (int32_t)rd32(buf.data() + roff[i]), ps = (int32_t)rd32(buf.data() + roff[i] + 4);
+                if (t < 0 || t > tid1 || (t == tid1 && (int64_t)ps >= end1)) {
+                    nr = i;
+                    done = true;
+                    p = roff[i] - 4;
+                    break;
+                }
+            }
         // prefix offsets, then pass 2 (parallel): copy into the columnar arrays
         const size_t base = b->pos.size();
         size_t kept = 0;

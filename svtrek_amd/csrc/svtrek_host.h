@@ -25,6 +25,14 @@ typedef struct svth_bam svth_bam;
 /* Read a BAM (BGZF) completely into a columnar pileup.  threads >= 1 inflate workers.
  * Returns NULL on error (message in err). */
 svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap);
+/* The records of a coordinate-sorted BAM from (tid0, beg0) up to, excluding, the first
+ * record at or past (tid1, end1), read from the BAI's linear-index offset of (tid0, beg0)
+ * (`path`.bai, required; the file's header is read from its start).  Every region query
+ * (tid, [beg, end)) with (tid0, beg0) <= (tid, beg) and (tid, end) <= (tid1, end1) yields the
+ * same reads from this pileup as from the whole file; a few records before beg0 may be
+ * included.  tid0 < 0: the whole file (svth_bam_read). */
+svth_bam *svth_bam_read_region(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
+                               char *err, size_t errcap);
 void      svth_bam_free(svth_bam *b);
 /* View valid until svth_bam_free. */
 void      svth_bam_view(const svth_bam *b, svt_pileup_view *out);
@@ -37,6 +45,22 @@ int64_t   svth_bam_n_cg_restored(const svth_bam *b); /* CIGARs restored from CG:
  * Returns 1 = record reaches the type switch (*l filled), 0 = skipped silently,
  * 2 = skipped with a stderr message (written into err). */
 int svth_parse_line(char *line, svt_locus *l, char *err, size_t errcap);
+
+/* A1 over a whole VCF text (the reader loop of process_vcf, audit.c:295-338: lines shorter
+ * than 2 bytes and '#' lines skipped, the trailing '\n' stripped), parsed by `threads`
+ * threads over '\n'-aligned pieces.  Records in file order; the stderr messages the
+ * reference's workers would print (parse errors, "[ERROR] Unkown type.") in file order. */
+typedef struct svth_vcf svth_vcf;
+svth_vcf        *svth_vcf_parse(const char *text, size_t len, int threads);
+size_t           svth_vcf_count(const svth_vcf *v);
+const svt_locus *svth_vcf_loci(const svth_vcf *v);
+const char      *svth_vcf_messages(const svth_vcf *v, size_t *len);
+void             svth_vcf_free(svth_vcf *v);
+
+/* A11 over a batch: the concatenated stdout text of n records in order, formatted by
+ * `threads` threads; malloc'ed (free with svth_free), *len = its length. */
+char *svth_format_batch(const svt_locus *l, const svt_result *r, size_t n, int threads, size_t *len);
+void  svth_free(void *p);
 
 /* A11: stdout text for one refined record; returns bytes written (0 = prints nothing:
  * DUP/TRA/BND/unknown -> "[ERROR] Unkown type." on stderr, or DEL/INV of exactly 50 bp). */

@@ -6,7 +6,11 @@
 //   print:  audit.c:176-232 printf formats (%u / %d of uint32 values, NA for 0xFFFFFFFF).
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
 
 #include "svtrek_host.h"
 
@@ -33,9 +37,103 @@ void info_value(const char *v, char *buf, size_t cap) {
     buf[len] = 0;
 }
 
+// [b, e) of the text split into `parts` pieces that start right after a '\n'
+std::vector<size_t> line_cuts(const char *text, size_t len, int parts) {
+    std::vector<size_t> cut{0};
+    for (int t = 1; t < parts; t++) {
+        size_t c = len * (size_t)t / (size_t)parts;
+        const void *nl = c < len ? memchr(text + c, '\n', len - c) : nullptr;
+        c = nl ? (size_t)((const char *)nl - text) + 1 : len;
+        cut.push_back(std::max(c, cut.back()));
+    }
+    cut.push_back(len);
+    return cut;
+}
+
+template <typename F>
+void run_parts(int parts, F &&f) {
+    if (parts <= 1) { f(0); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < parts; t++) th.emplace_back([&, t] { f(t); });
+    for (auto &x : th) x.join();
+}
+
 }  // namespace
 
+struct svth_vcf {
+    std::vector<svt_locus> loci;
+    std::string msgs;
+};
+
 extern "C" {
+
+svth_vcf *svth_vcf_parse(const char *text, size_t len, int threads) {
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), len / (1u << 20) + 1));
+    const std::vector<size_t> cut = line_cuts(text, len, T);
+    std::vector<svth_vcf> part((size_t)T);
+    run_parts(T, [&](int t) {
+        svth_vcf &o = part[(size_t)t];
+        std::string line;
+        char perr[1024];
+        for (size_t i = cut[(size_t)t], e = cut[(size_t)t + 1]; i < e;) {
+            const void *nl = memchr(text + i, '\n', e - i);
+            const size_t n = (nl ? (size_t)((const char *)nl - text) + 1 : e) - i;
+            const char *ln = text + i;
+            i += n;
+            if (n < 2 || ln[0] == '#') continue;                 // audit.c:324-325
+            line.assign(ln, ln[n - 1] == '\n' ? n - 1 : n);     // :327-330
+            svt_locus l;
+            const int act = svth_parse_line(&line[0], &l, perr, sizeof perr);
+            if (act == 2) o.msgs += perr;
+            if (act != 1) continue;
+            if (svth_is_unknown_type(&l)) o.msgs += "[ERROR] Unkown type.\n";
+            o.loci.push_back(l);
+        }
+    });
+    svth_vcf *v = new svth_vcf();
+    size_t n = 0;
+    for (auto &p : part) n += p.loci.size();
+    v->loci.reserve(n);
+    for (auto &p : part) {
+        v->loci.insert(v->loci.end(), p.loci.begin(), p.loci.end());
+        v->msgs += p.msgs;
+    }
+    return v;
+}
+
+size_t svth_vcf_count(const svth_vcf *v) { return v->loci.size(); }
+const svt_locus *svth_vcf_loci(const svth_vcf *v) { return v->loci.data(); }
+const char *svth_vcf_messages(const svth_vcf *v, size_t *len) {
+    if (len) *len = v->msgs.size();
+    return v->msgs.c_str();
+}
+void svth_vcf_free(svth_vcf *v) { delete v; }
+
+char *svth_format_batch(const svt_locus *l, const svt_result *r, size_t n, int threads, size_t *len) {
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), n / 16384 + 1));
+    std::vector<std::string> part((size_t)T);
+    run_parts(T, [&](int t) {
+        std::string &o = part[(size_t)t];
+        const size_t b = n * (size_t)t / (size_t)T, e = n * (size_t)(t + 1) / (size_t)T;
+        o.reserve((e - b) * 128);
+        char buf[512];
+        for (size_t k = b; k < e; k++) {
+            const int m = svth_format(&l[k], &r[k], buf, sizeof buf);
+            if (m > 0) o.append(buf, (size_t)m);
+        }
+    });
+    size_t tot = 0;
+    for (auto &p : part) tot += p.size();
+    char *out = (char *)malloc(tot + 1);
+    if (!out) return nullptr;
+    size_t at = 0;
+    for (auto &p : part) { memcpy(out + at, p.data(), p.size()); at += p.size(); }
+    out[tot] = 0;
+    if (len) *len = tot;
+    return out;
+}
+
+void svth_free(void *p) { free(p); }
 
 int svth_parse_line(char *line, svt_locus *l, char *err, size_t errcap) {
     char *save = nullptr, *alt_save = nullptr;

@@ -22,6 +22,23 @@ def load_host() -> C.CDLL:
         P = C.c_void_p
         L.svth_bam_read.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_size_t]
         L.svth_bam_read.restype = P
+        L.svth_bam_read_region.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int64, C.c_int32, C.c_int64,
+                                           C.c_char_p, C.c_size_t]
+        L.svth_bam_read_region.restype = P
+        L.svth_vcf_parse.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
+        L.svth_vcf_parse.restype = P
+        L.svth_vcf_count.argtypes = [P]
+        L.svth_vcf_count.restype = C.c_size_t
+        L.svth_vcf_loci.argtypes = [P]
+        L.svth_vcf_loci.restype = P
+        L.svth_vcf_messages.argtypes = [P, C.POINTER(C.c_size_t)]
+        L.svth_vcf_messages.restype = P
+        L.svth_vcf_free.argtypes = [P]
+        L.svth_vcf_free.restype = None
+        L.svth_format_batch.argtypes = [P, P, C.c_size_t, C.c_int, C.POINTER(C.c_size_t)]
+        L.svth_format_batch.restype = P
+        L.svth_free.argtypes = [P]
+        L.svth_free.restype = None
         L.svth_bam_free.argtypes = [P]
         L.svth_bam_free.restype = None
         L.svth_bam_view.argtypes = [P, C.POINTER(SvtPileupView)]
@@ -44,10 +61,17 @@ def load_host() -> C.CDLL:
     return _host
 
 
-def read_bam(path: str, threads: int = 4) -> tuple[Pileup, dict]:
+def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | None = None) -> tuple[Pileup, dict]:
+    """The BAM as a columnar pileup.  region = (tid0, beg0, tid1, end1): only the records from
+    the BAI's linear-index offset of (tid0, beg0) up to the first at or past (tid1, end1)
+    (svth_bam_read_region; needs `path`.bai) -- what one shard's queries can yield."""
     L = load_host()
     err = C.create_string_buffer(512)
-    h = L.svth_bam_read(path.encode(), threads, err, 512)
+    if region is None:
+        h = L.svth_bam_read(path.encode(), threads, err, 512)
+    else:
+        t0, b0, t1, e1 = (int(x) for x in region)
+        h = L.svth_bam_read_region(path.encode(), threads, t0, b0, t1, e1, err, 512)
     if not h:
         raise OSError(err.value.decode())
     try:
@@ -86,6 +110,41 @@ def parse_line(line: str):
     act = L.svth_parse_line(buf, loc.ctypes.data, err, 1024)
     rec = tuple(int(x) for x in loc[0]) if act == 1 else None
     return act, rec, err.value.decode("latin-1")
+
+
+def parse_vcf_text(data: bytes, threads: int = 4) -> tuple[np.ndarray, str]:
+    """A1 over a whole VCF (svth_vcf_parse, multithreaded): (loci in file order, the stderr
+    text the reference's workers print for skipped / unknown records, in file order)."""
+    L = load_host()
+    h = L.svth_vcf_parse(data, len(data), threads)
+    if not h:
+        raise MemoryError("svth_vcf_parse failed")
+    try:
+        n = int(L.svth_vcf_count(h))
+        loci = np.zeros(n, dtype=LOCUS_DTYPE)
+        if n:
+            C.memmove(loci.ctypes.data, L.svth_vcf_loci(h), n * LOCUS_DTYPE.itemsize)
+        ml = C.c_size_t(0)
+        mp = L.svth_vcf_messages(h, C.byref(ml))
+        msgs = C.string_at(mp, ml.value).decode("latin-1") if ml.value else ""
+        return loci, msgs
+    finally:
+        L.svth_vcf_free(h)
+
+
+def format_batch(loci: np.ndarray, res: np.ndarray, threads: int = 4) -> str:
+    """A11 of every record, in order (svth_format_batch, multithreaded)."""
+    L = load_host()
+    loci = np.ascontiguousarray(loci)
+    res = np.ascontiguousarray(res)
+    n = C.c_size_t(0)
+    p = L.svth_format_batch(loci.ctypes.data, res.ctypes.data, len(loci), threads, C.byref(n))
+    if not p:
+        raise MemoryError("svth_format_batch failed")
+    try:
+        return C.string_at(p, n.value).decode("latin-1")
+    finally:
+        L.svth_free(p)
 
 
 def format_result(locus: np.void, result: np.void) -> str:

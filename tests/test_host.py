@@ -163,3 +163,61 @@ def test_format_examples():
     # a DEL of exactly 50 bp reaches the switch but prints nothing (audit.c:190)
     loc = np.array([(2, 1, 100, 150)], dtype=LOCUS_DTYPE)[0]
     assert host.format_result(loc, np.array([(SVT_NA, SVT_NA)], dtype=RESULT_DTYPE)[0]) == ""
+
+
+@pytest.mark.parametrize("region", [(0, 30000, 0, 90000), (0, 50000, 2, 40000), (1, 0, 1, 1 << 30),
+                                    (2, 10 ** 8, 2, 10 ** 8 + 5)])
+def test_bam_region_read(tmp_path, region):
+    """svth_bam_read_region (BAI linear-index seek): every query inside the region yields
+    the same reads as from the whole file, and the read stops at the region end."""
+    from svtrek_amd.pileup import Pileup  # noqa: F401
+    cfg = sim.SimConfig(seed=31, n_targets=3, n_loci=60, del_frac=0.5, coverage=10.0, p_clip_ends=0.3)
+    r = sim.generate(cfg, keep_handle=True)
+    path = str(tmp_path / "r.bam")
+    sim.write_bam(r, path, with_seq=True, level=1)
+    full, _ = host.read_bam(path, threads=2)
+    part, info = host.read_bam(path, threads=2, region=region)
+    t0, b0, t1, e1 = region
+    tids = np.repeat(np.arange(3), np.diff(full.tid_off))
+    pt = np.repeat(np.arange(3), np.diff(part.tid_off))
+    # nothing at or past the region end; every full-file record overlapping the region is there
+    assert not ((pt > t1) | ((pt == t1) & (part.pos >= e1))).any()
+    inside = ((tids > t0) | ((tids == t0) & (full.endpos > b0))) & ((tids < t1) | ((tids == t1) & (full.pos < e1)))
+    key = lambda t, p, e: set(zip(t.tolist(), p.tolist(), e.tolist()))
+    assert key(tids[inside], full.pos[inside], full.endpos[inside]) <= key(pt, part.pos, part.endpos)
+    assert info["records"] >= int(inside.sum())
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_vcf_batch_parse_and_format(threads):
+    """svth_vcf_parse / svth_format_batch (multithreaded, '\\n'-aligned pieces) give the
+    per-line parse's records and messages and the per-record text, in file order."""
+    import random
+    rng = random.Random(threads)
+    lines = [_fuzz_line(rng) for _ in range(3000)]
+    extra = ["", "#comment", "x", "1\t100\t.\tA\t<DEL>\t.\tPASS\tSVTYPE=DUP;END=900", "1\t0x\t.\tA\tT\t.\t.\tEND=5"]
+    lines += extra * 50
+    rng.shuffle(lines)
+    text = ("\n".join(lines) + "\n").encode("latin-1") * 3
+    loci, msgs = host.parse_vcf_text(text, threads=threads)
+    want, wmsg = [], []
+    for raw in text.decode("latin-1").split("\n"):
+        line = raw
+        if len(line) + 1 < 2 or line.startswith("#"):
+            continue
+        act, rec, err = host.parse_line(line)
+        if act == 2:
+            wmsg.append(err)
+        if act == 1:
+            if rec[0] not in (1, 2, 3):
+                wmsg.append("[ERROR] Unkown type.\n")
+            want.append(rec)
+    assert [tuple(int(x) for x in r) for r in loci] == want
+    assert msgs == "".join(wmsg)
+    rng2 = np.random.default_rng(threads)
+    from svtrek_amd._lib import RESULT_DTYPE
+    res = np.zeros(len(loci), dtype=RESULT_DTYPE)
+    res["start"] = np.where(rng2.random(len(loci)) < 0.3, 0xFFFFFFFF, rng2.integers(0, 2**32, len(loci)))
+    res["end"] = np.where(rng2.random(len(loci)) < 0.3, 0xFFFFFFFF, rng2.integers(0, 2**32, len(loci)))
+    assert host.format_batch(loci, res, threads=threads) == "".join(
+        host.format_result(loci[k], res[k]) for k in range(len(loci)))
