@@ -3,13 +3,16 @@
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         -m svtrek_amd.audt_dist -b sample.bam -v calls.vcf [--wider-interval N ...]
 
-Every rank reads the BAM into a columnar pileup, takes the contiguous slice
-[r*ceil(N/G), (r+1)*ceil(N/G)) of the loci in genomic order, uploads only the reads its
-queries can reach (pileup.halo_slice) and refines them on its own GPU
-(svtrek_amd.Engine, HIP); rank 0 gathers the 16-byte {vcf_index, start, end, pad}
-records (torch.distributed nccl = RCCL over xGMI) and prints the reference's stdout
-(A11) in VCF order.  Single-node `svtrek audt --gpus N` does the
-same sharding with host threads instead of processes.
+Every rank parses the VCF (svth_vcf_parse, multithreaded), takes the contiguous slice
+[r*ceil(N/G), (r+1)*ceil(N/G)) of the loci in genomic order and reads from the BAM only what
+that slice's queries can reach: the records from the BAI's linear-index offset of the
+slice's first query to its last query's end (svth_bam_read_region; the whole file when there
+is no BAI), trimmed to the queries' hull (pileup.halo_slice).  It refines them on its own GPU
+(svtrek_amd.Engine, HIP); the ranks agree on success with one all-reduce of a status flag
+(a rank that failed makes every rank exit non-zero instead of leaving the others blocked in
+the gather), then rank 0 gathers the 16-byte {vcf_index, start, end, pad} records
+(torch.distributed nccl = RCCL over xGMI) and prints the reference's stdout (A11) in VCF
+order.  Single-node `svtrek audt --gpus N` does the same sharding with host threads.
 """
 from __future__ import annotations
 
@@ -20,33 +23,74 @@ import sys
 import numpy as np
 
 
-def parse_vcf(path: str):
-    """A1 over every data line (audit.c:301-338) via the C++ parser; returns (loci, stderr lines)."""
+def parse_vcf(path: str, threads: int = 4):
+    """A1 over every data line (audit.c:301-338) via the C++ batch parser: (loci, stderr text)."""
     from . import host
-    from ._lib import LOCUS_DTYPE
-    rows, errs = [], []
     with open(path, "rb") as f:
-        data = f.read().decode("latin-1")
-    i = 0
-    while i < len(data):
-        j = data.find("\n", i)
-        line = data[i:] if j < 0 else data[i:j + 1]
-        i += len(line)
-        if len(line) < 2 or line[0] == "#":
-            continue
-        if line.endswith("\n"):
-            line = line[:-1]
-        act, rec, err = host.parse_line(line)
-        if act == 2:
-            errs.append(err)
-        if act == 1:
-            if rec[0] not in (1, 2, 3):
-                errs.append("[ERROR] Unkown type.\n")
-            rows.append(rec)
-    loci = np.zeros(len(rows), dtype=LOCUS_DTYPE)
-    for k, r in enumerate(rows):
-        loci[k] = r
-    return loci, errs
+        data = f.read()
+    return host.parse_vcf_text(data, threads=threads)
+
+
+def shard_region(loci: np.ndarray, wider: int, median: int, narrow: int):
+    """(tid0, beg0, tid1, end1) spanning every query of `loci` (one genomic-order shard), or
+    None when they issue none: the part of a sorted BAM svth_bam_read_region has to read."""
+    from .pileup import query_spans
+    if len(loci) == 0:
+        return None
+    nt = int(max(1, int(loci["chrom"].max())))
+    sp = query_spans(loci, wider, median, narrow, nt)
+    live = np.nonzero(sp[:, 1] > sp[:, 0])[0]
+    if len(live) == 0:
+        return None
+    t0, t1 = int(live[0]), int(live[-1])
+    return t0, int(sp[t0, 0]), t1, int(sp[t1, 1])
+
+
+def load_shard(bam: str, loci: np.ndarray, prm, threads: int):
+    """The reads the shard's queries can yield: a BAI region read + halo trim (or, without a
+    BAI, the whole file + halo trim)."""
+    from . import host
+    from .pileup import halo_slice
+    reg = shard_region(loci, prm.wider_interval, prm.median_interval, prm.narrow_interval)
+    if reg is None:
+        reg = (0, 0, 0, 0)
+    if os.path.exists(bam + ".bai"):
+        pl, info = host.read_bam(bam, threads=threads, region=reg)
+    else:
+        sys.stderr.write(f"[svtrek_amd] no {bam}.bai: reading the whole BAM\n")
+        pl, info = host.read_bam(bam, threads=threads)
+    return halo_slice(pl, loci, prm.wider_interval, prm.median_interval, prm.narrow_interval), info
+
+
+def run_rank(bam: str, loci: np.ndarray, prm, threads: int, refine, world: int, rank: int, device=None):
+    """One rank's whole job: shard, region load, refine (refine(pileup, loci) -> results),
+    status agreement, gather.  Returns every result in VCF order on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    from ._lib import RESULT_DTYPE
+    from .distributed import gather_results, shard_rows
+    rows = shard_rows(loci, world, rank)
+    mine = loci[rows]
+    err = None
+    local = np.zeros(0, dtype=RESULT_DTYPE)
+    try:
+        if len(rows):
+            pl, _ = load_shard(bam, mine, prm, threads)
+            local = refine(pl, mine)
+    except Exception as e:   # noqa: BLE001 -- reported, then every rank stops together
+        err = f"rank {rank}: {type(e).__name__}: {e}"
+    if world > 1:
+        flag = torch.tensor([1 if err else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if int(flag.item()):
+            raise RuntimeError(err or f"rank {rank}: another rank failed")
+        return gather_results(rows, local, len(loci), device=device)
+    if err:
+        raise RuntimeError(err)
+    out = np.empty(len(loci), dtype=RESULT_DTYPE)
+    out[rows] = local
+    return out
 
 
 def main(argv=None) -> int:
@@ -66,8 +110,6 @@ def main(argv=None) -> int:
     import torch.distributed as dist
 
     from . import Engine, Params, host
-    from .distributed import gather_results, shard_rows
-    from .pileup import halo_slice
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -78,32 +120,29 @@ def main(argv=None) -> int:
         dist.init_process_group("nccl", device_id=dev)
     if rank == 0:
         sys.stdout.write("[INFO] Started processing variation file.\n")
-    loci, errs = parse_vcf(a.vcf)
-    if rank == 0:
-        for e in errs:
-            sys.stderr.write(e)
-    pileup, _ = host.read_bam(a.bam, threads=max(1, a.t))
+        sys.stdout.flush()
+    loci, msgs = parse_vcf(a.vcf, threads=max(1, a.t))
+    if rank == 0 and msgs:
+        sys.stderr.write(msgs)
     prm = Params(a.wider_interval, a.median_interval, a.narrow_interval, a.consensus_interval_range,
                  a.consensus_interval, a.consensus_min_count)
+    rc = 0
     with Engine(prm, device=local) as eng:
-        if world > 1:
-            rows = shard_rows(loci, world, rank)
-            mine = loci[rows]
-            eng.load_pileup(halo_slice(pileup, mine, a.wider_interval, a.median_interval, a.narrow_interval))
-            del pileup
-            local_res = eng.refine(mine)
-            res = gather_results(rows, local_res, len(loci), device=dev)
-        else:
-            eng.load_pileup(pileup)
-            res = eng.refine(loci)
-    if rank == 0:
-        out = [host.format_result(loci[k], res[k]) for k in range(len(loci))]
-        sys.stdout.write("".join(out))
+        def refine(pl, mine):
+            eng.load_pileup(pl)
+            return eng.refine(mine)
+        try:
+            res = run_rank(a.bam, loci, prm, max(1, a.t), refine, world, rank, device=dev)
+        except RuntimeError as e:
+            sys.stderr.write(f"[ERROR] {e}\n")
+            res, rc = None, 1
+    if rank == 0 and rc == 0:
+        sys.stdout.write(host.format_batch(loci, res, threads=max(1, a.t)))
         sys.stdout.write("[INFO] Ended processing variation file\n")
         sys.stdout.flush()
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

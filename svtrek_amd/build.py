@@ -98,6 +98,37 @@ def build_oracle(force: bool = False) -> str:
     return out
 
 
+SAN_FLAGS = {"asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
+             "tsan": ["-fsanitize=thread"]}
+
+
+def build_sanitizers(force: bool = False) -> dict[str, str]:
+    """Test artefacts (host code only, tests/test_sanitizers.py): the product's host C++
+    (bam_ingest.cpp, vcf_audit.cpp) and the oracle's threaded paths, each under ASan+UBSan
+    and under TSan, as standalone drivers (tests/san/) in build/san/."""
+    out_dir = os.path.join(ROOT, "build", "san")
+    os.makedirs(out_dir, exist_ok=True)
+    host_src = [os.path.join(ROOT, "tests", "san", "host_san.cpp")] + \
+        [os.path.join(CSRC, f) for f in ("bam_ingest.cpp", "vcf_audit.cpp")]
+    orc_src = [os.path.join(ROOT, "tests", "san", "oracle_san.c"), os.path.join(CSRC, "simpileup.c")] + \
+        [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "poa_oracle.c", "bgzf_ref.c")]
+    hdrs = [os.path.join(CSRC, "svtrek_host.h"), os.path.join(INC, "svtrek_gpu.h"), os.path.join(CSRC, "simpileup.h"),
+            os.path.join(ROOT, "oracle", "svtrek_oracle.h")]
+    arts = {}
+    for kind, fl in SAN_FLAGS.items():
+        out = os.path.join(out_dir, f"host_{kind}")
+        if force or _stale(out, host_src + hdrs):
+            _run(["g++", "-O1", "-g", "-std=c++17", "-pthread", *fl, "-I", INC, "-I", CSRC, "-o", out] + host_src +
+                 ["-lz", "-ldl"])
+        arts[f"host_{kind}"] = out
+        out = os.path.join(out_dir, f"oracle_{kind}")
+        if force or _stale(out, orc_src + hdrs):
+            _run(["gcc", "-O1", "-g", "-std=gnu11", "-pthread", *fl, "-I", CSRC, "-I", os.path.join(ROOT, "oracle"),
+                  "-o", out] + orc_src + ["-lz", "-lm"])
+        arts[f"oracle_{kind}"] = out
+    return arts
+
+
 def build_all(force: bool = False) -> dict[str, str]:
     arts = {
         "engine": build_engine(force),

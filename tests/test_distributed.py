@@ -164,3 +164,60 @@ def test_gloo_bench_shard_and_gather_path(tmp_path, world):
     recs = np.load(tmp_path / "recs.npy")
     got = unpack_records(recs, len(r.loci))
     np.testing.assert_array_equal(got.view(np.uint32), O.refine_batch(r.pileup, r.loci).view(np.uint32))
+
+
+def _audt_worker(rank, world, port, bam, outdir, fail_rank):
+    """audt_dist.run_rank on gloo: BAI region read + halo trim per rank, status all-reduce,
+    gather; the oracle stands in for the GPU engine (test infrastructure)."""
+    import torch.distributed as dist
+
+    import oracle_ffi as O
+    from svtrek_amd import Params, audt_dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    loci, _ = audt_dist.parse_vcf(os.path.join(outdir, "c.vcf"), threads=2)
+    seen = {}
+
+    def refine(pl, mine):
+        if rank == fail_rank:
+            raise ValueError("injected failure")
+        seen["reads"] = pl.n_reads
+        return O.refine_batch(pl, mine)
+
+    try:
+        res = audt_dist.run_rank(bam, loci, Params(), 2, refine, world, rank)
+        if rank == 0:
+            np.save(os.path.join(outdir, "res.npy"), res.view(np.uint32).reshape(-1, 2))
+        np.save(os.path.join(outdir, f"reads{rank}.npy"), np.array([seen.get("reads", 0)]))
+    except RuntimeError as e:
+        with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+            f.write(str(e))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, -1), (3, -1), (2, 1)])
+def test_gloo_audt_dist_region_shards(tmp_path, world, fail_rank):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
+    import oracle_ffi as O
+    from svtrek_amd import sim
+    r = sim.generate(sim.SimConfig(seed=23, n_loci=120, n_targets=3, del_frac=0.5, coverage=10), keep_handle=True)
+    bam = str(tmp_path / "c.bam")
+    sim.write_bam(r, bam, with_seq=True, level=1)
+    sim.write_vcf(r.loci, str(tmp_path / "c.vcf"))
+    mp.spawn(_audt_worker, args=(world, _free_port(), bam, str(tmp_path), fail_rank), nprocs=world, join=True)
+    if fail_rank >= 0:   # every rank stops with an error, none hangs in the gather
+        for k in range(world):
+            assert (tmp_path / f"err{k}.txt").exists()
+        assert "injected failure" in (tmp_path / f"err{fail_rank}.txt").read_text()
+        return
+    from svtrek_amd import audt_dist
+    loci, _ = audt_dist.parse_vcf(str(tmp_path / "c.vcf"))
+    want = O.refine_batch(r.pileup, loci).view(np.uint32).reshape(-1, 2)
+    np.testing.assert_array_equal(np.load(tmp_path / "res.npy"), want)
+    reads = [int(np.load(tmp_path / f"reads{k}.npy")[0]) for k in range(world)]
+    assert max(reads) < r.pileup.n_reads   # each rank read only its region of the BAM
