@@ -131,7 +131,13 @@ def load_engine() -> C.CDLL:
             import torch  # noqa: F401
         except ImportError:
             pass
-    lib = C.CDLL(path)
+    _engine = bind_abi(C.CDLL(path))
+    return _engine
+
+
+def bind_abi(lib: C.CDLL) -> C.CDLL:
+    """Declare include/svtrek_gpu.h's entry points on a loaded library (the HIP engine; the
+    tests also bind oracle/libsvtrek_cpu.so, the CPU restatement behind the same header)."""
     P = C.c_void_p
     lib.svt_open.argtypes = [C.POINTER(SvtParams), C.c_int, C.POINTER(P)]
     lib.svt_open_multi.argtypes = [C.POINTER(SvtParams), C.c_int, P, C.POINTER(P)]
@@ -165,7 +171,6 @@ def load_engine() -> C.CDLL:
     for name in ("svt_open", "svt_open_multi", "svt_refine_device_records", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
                  "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):
         getattr(lib, name).restype = C.c_int32
-    _engine = lib
     return lib
 
 

@@ -92,9 +92,18 @@ def build_sim(force: bool = False) -> str:
 def build_oracle(force: bool = False) -> str:
     """Test infrastructure: the CPU parity oracle (oracle/Makefile)."""
     out = os.path.join(ROOT, "oracle", "liboracle.so")
-    src = [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "poa_oracle.c", "bgzf_ref.c", "svtrek_oracle.h", "Makefile")]
-    if force or _stale(out, src):
+    src = [os.path.join(ROOT, "oracle", f) for f in ("svtrek_oracle.c", "poa_oracle.c", "bgzf_ref.c", "svtrek_oracle.h",
+                                                      "svtrek_cpu.c", "Makefile")] + [os.path.join(INC, "svtrek_gpu.h")]
+    cpu = os.path.join(ROOT, "oracle", "libsvtrek_cpu.so")
+    if force or _stale(out, src) or _stale(cpu, src):
         _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + (["-B"] if force else []))
+    # the product's CLI (svtrek_main.cpp) linked against the CPU backend: CPU-side CLI tests
+    cli = os.path.join(ROOT, "oracle", "_cpu", "svtrek_cpu")
+    csrc = [os.path.join(CSRC, f) for f in ("svtrek_main.cpp", "bam_ingest.cpp", "vcf_audit.cpp")]
+    if os.path.exists(csrc[0]) and (force or _stale(cli, csrc + [cpu, os.path.join(CSRC, "svtrek_host.h")])):
+        os.makedirs(os.path.dirname(cli), exist_ok=True)
+        _run(["g++", "-O2", "-std=c++17", "-pthread", "-I", INC, "-o", cli] + csrc +
+             ["-L", os.path.join(ROOT, "oracle"), "-lsvtrek_cpu", "-Wl,-rpath,$ORIGIN/..", "-lz", "-ldl"])
     return out
 
 

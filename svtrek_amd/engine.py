@@ -51,10 +51,14 @@ class SvtError(RuntimeError):
 class Engine:
     """One GPU context (svt_ctx).  Use one Engine per process/GPU."""
 
-    def __init__(self, params: Params | None = None, device: int = -1, devices: list[int] | None = None):
+    def __init__(self, params: Params | None = None, device: int = -1, devices: list[int] | None = None,
+                 lib: C.CDLL | None = None):
         """One context on `device` (-1 = current), or -- with `devices` -- one context over
-        several GPUs (svt_open_multi: the pileup is replicated, host batches are split)."""
-        self.lib = load_engine()
+        several GPUs (svt_open_multi: the pileup is replicated, host batches are split).
+        lib: another library implementing include/svtrek_gpu.h, bound with _lib.bind_abi --
+        only the tests pass one (oracle/libsvtrek_cpu.so, the CPU restatement, to run the
+        same calls on both backends); by default the HIP engine, which must be built."""
+        self.lib = lib if lib is not None else load_engine()
         self.params = params or Params()
         self._cp = self.params.to_c()
         h = C.c_void_p()

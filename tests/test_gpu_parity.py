@@ -367,3 +367,26 @@ def test_vote_band_edges(engine_factory, seed):
     got = eng.refine(loci)
     want = O.refine_batch(pl, loci, eng.params)
     _assert_same(got, want, loci)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_hip_and_cpu_backends_through_one_abi(engine_factory, seed):
+    """The same svt_open / svt_load_pileup / svt_refine_batch / svt_count_work calls on the
+    HIP engine and on oracle/libsvtrek_cpu.so (the CPU restatement behind include/svtrek_gpu.h)."""
+    import ctypes as C
+    import os
+
+    from svtrek_amd._lib import bind_abi
+    cpu_lib = bind_abi(C.CDLL(os.path.join(os.path.dirname(O.__file__), "libsvtrek_cpu.so")))
+    rng = np.random.default_rng(900 + seed)
+    hot = [int(x) for x in rng.integers(5000, 55000, size=6)]
+    pl = random_pileup(rng, n_targets=2, contig_len=60000, n_reads=int(rng.integers(100, 600)), max_ops=120, hot=hot)
+    loci = random_loci(rng, 400, 2, 60000, hot)
+    gpu = engine_factory()
+    gpu.load_pileup(pl)
+    with Engine(Params(), device=0, lib=cpu_lib) as cpu:
+        cpu.load_pileup(pl)
+        _assert_same(gpu.refine(loci), cpu.refine(loci), loci)
+        wc, wg = cpu.count_work(loci), gpu.count_work(loci)
+        assert (wc["windows"], wc["reads"], wc["ops_walked"], wc["candidates"]) == \
+            (wg["windows"], wg["reads"], wg["ops_walked"], wg["candidates"])
