@@ -284,7 +284,7 @@ def main() -> int:
     ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
     ref_ms = kern_mean_ms + load_stats["index_ms"]
     gather_variant = os.environ.get("SVTREK_GATHER", "span")
-    kernel = {"span": "refine_span_kernel", "event": "refine_event_kernel",
+    kernel = {"span": "refine_lane_kernel", "span1": "refine_span_kernel", "event": "refine_event_kernel",
               "index": "refine_index_kernel"}.get(gather_variant, "refine_kernel")
     traffic, traffic_src = _traffic(args.workload, kernel, records=True)
     if args.scale != 1.0 or world > 1:

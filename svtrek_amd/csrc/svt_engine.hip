@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.9.4 (gfx950, span walk, band vote)"
+#define SVT_VERSION "svtrek_amd 0.10.0 (gfx950, span walk, lane vote)"
 
 namespace {
 
@@ -1179,29 +1179,76 @@ __device__ __forceinline__ void span_count(const DevPileup &P, int tid, uint32_t
     }
 }
 
+// read_range (A3) with the span bounds read in the same dependent step as the pos/emax
+// probes: each probe lane also loads the span offset and slow-read prefix of its read, and
+// the bounds are taken from the lanes where the two searches end (one HBM round trip less
+// per window).  Wider bucket ranges fall back to read_range + one more step.
+template <int KIND>
+__device__ __forceinline__ bool span_query(const DevPileup &P, int tid, int64_t beg, int64_t end, int64_t &lo,
+                                           int64_t &hi, uint64_t &E0, uint64_t &E1, uint64_t &nslow) {
+    if (tid < 0 || tid >= P.n_targets || end <= beg) return false;   // no reads (A3)
+    const int64_t ra = P.tid_off[tid], nr = P.tid_off[tid + 1] - ra;
+    if (nr == 0) return false;
+    const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
+    const int64_t b0 = P.bkt_off[tid], nb = P.bkt_off[tid + 1] - b0;   // last bucket = {nr, nr}
+    const int ln = lane_id();
+    const int64_t bi = min((ln < 2 ? end >> BKT_SHIFT : beg >> BKT_SHIFT) + (ln & 1), nb - 1);
+    const uint2 bw = ln < 4 ? P.bkt[b0 + bi] : make_uint2(0, 0);
+    const int64_t hl = rdlane(bw.x, 0), hh = rdlane(bw.x, 1), ll = rdlane(bw.y, 2), lh = rdlane(bw.y, 3);
+    if (hh - hl >= WAVE || lh - ll >= WAVE) {   // wide bucket: the general search, then the bounds
+        if (!read_range(P, tid, beg, end, lo, hi)) return false;
+        const uint64_t ob = ln < 2 ? off[ln ? hi : lo] : ln < 4 ? P.slowpre[ln == 3 ? hi : lo] : 0ull;
+        E0 = rdlane64(ob, 0);
+        E1 = rdlane64(ob, 1);
+        nslow = rdlane64(ob, 3) - rdlane64(ob, 2);
+        return true;
+    }
+    // lanes [0, hh-hl] cover the hi candidates hl .. hh, lanes [0, lh-ll] the lo candidates
+    const bool vh = hl + ln <= hh, vl = ll + ln <= lh;
+    const int64_t rh = ra + (vh ? hl + ln : hl), rl = ra + (vl ? ll + ln : ll);
+    const int32_t pv = vh && hl + ln < hh ? P.pos[rh] : 0, ev = vl && ll + ln < lh ? P.emax[rl] : 0;
+    const uint64_t oh = off[rh], ol = off[rl];
+    const uint64_t sh = P.slowpre[rh], sl = P.slowpre[rl];
+    const uint64_t mh = ballot(vh && hl + ln < hh && (int64_t)pv >= end);
+    const uint64_t ml = ballot(vl && ll + ln < lh && (int64_t)ev > beg);
+    const int kh = mh ? __builtin_ctzll(mh) : (int)(hh - hl), kl = ml ? __builtin_ctzll(ml) : (int)(lh - ll);
+    hi = ra + hl + kh;
+    lo = ra + ll + kl;
+    if (lo >= hi) return false;
+    E1 = rdlane64(oh, kh);
+    E0 = rdlane64(ol, kl);
+    nslow = rdlane64(sh, kh) - rdlane64(sl, kl);
+    return true;
+}
+
 // The span walk proper: events [E0, E1) of the yielded reads [lo, hi) of window [s, e]
 // (query beg = s-1), nslow = the slow reads among them.  Leaves the candidate count in
 // *sink.cnt.
 template <int KIND>
 __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t s, uint32_t e, int64_t lo, int64_t hi,
-                                          uint64_t E0, uint64_t E1, uint64_t nslow, Sink &sink) {
+                                          uint64_t E0, uint64_t E1, uint64_t nslow, Sink &sink,
+                                          uint64_t cbase_in = ~0ull) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u);
     const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);   // read_range yielded reads: beg < end <= 2^31 - 1
     const int ln = lane_id();
     const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
-    const uint64_t cbase = KIND == K_END ? P.off64[P.tid_off[tid]] : 0ull;   // stop searches' arena base
+    // the stop searches' arena base: the contig's first arena offset (given, or loaded here)
+    const uint64_t cbase = KIND != K_END ? 0ull : cbase_in != ~0ull ? cbase_in : P.off64[P.tid_off[tid]];
     int32_t cnt = 0;   // candidates appended so far (wave-uniform)
     for (uint64_t b = E0; b < E1; b += SPAN_U * WAVE) {
         uint4 v[SPAN_U];
         const uint64_t left = E1 - b;   // events from b on (wave-uniform): the u-slots past them are skipped
+        // loads with clamped indices and no branches, so that all of them are in flight
+        // before the first is used; lanes past E1 are masked below
 #pragma unroll
         for (int u = 0; u < SPAN_U; u++) {
             const uint64_t j = b + (uint64_t)(u * WAVE + ln);
-            v[u] = j < E1 ? ev[j] : make_uint4(0, 0, 0, 0);   // zero event: op M, endpos 0 -> no candidate
+            if ((uint64_t)(u * WAVE) < left) v[u] = ev[j < E1 ? j : E1 - 1];
         }
 #pragma unroll
         for (int u = 0; u < SPAN_U; u++) {
             if ((uint64_t)(u * WAVE) >= left) break;
+            if ((uint64_t)(u * WAVE + ln) >= left) v[u] = make_uint4(0, 0, 0, 0);   // zero event: no candidate
             const uint32_t x = v[u].x, op = v[u].y & 0xfu, len = v[u].y >> 4;
             const bool ovl = (int32_t)v[u].z > beg32;   // hts_itr_next overlap; pos < end holds below hi
             bool c, brk = false;
@@ -1264,15 +1311,11 @@ __device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_
     if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi)) return;
+    uint64_t E0, E1, nslow;
+    if (!span_query<KIND>(P, tid, beg, end, lo, hi, E0, E1, nslow)) return;
 #if SVT_DIAG == 1
     if (lo < hi) return;     // diagnostic build: region query only
 #endif
-    const int ln = lane_id();
-    const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
-    // one step: the span bounds (lanes 0, 1) and the slow-read count of [lo, hi) (lanes 2, 3)
-    const uint64_t ob = ln < 2 ? off[ln ? hi : lo] : ln < 4 ? P.slowpre[ln == 3 ? hi : lo] : 0ull;
-    const uint64_t E0 = rdlane64(ob, 0), E1 = rdlane64(ob, 1), nslow = rdlane64(ob, 3) - rdlane64(ob, 2);
     span_walk<KIND>(P, tid, s, e, lo, hi, E0, E1, nslow, sink);
 }
 
@@ -1910,6 +1953,318 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
     }
 }
 
+// ------------------------------------------------------------------ lane-vote kernel
+// The default timed kernel.  A wave takes LV_W consecutive windows.  Phase 1, per window
+// and wave-wide: the A2 window, the span query and walk (A3-A7) and the exact band filter
+// (band_filter); a window whose band holds <= LV_CAP elements, all >= 0, within +-1023 of
+// pos (the common case: ~20 candidates of its own breakpoint) is staged in LDS as 16-bit
+// offsets from the band's low end, with the band's three whole-multiset facts.  Phase 2,
+// one LANE per staged window: an in-register sorting network over the lane's offsets,
+// 16-bit prefix sums, and consensus_pos (refinement.c:41-101) run per lane as the
+// reference's own loops -- with the cluster starts/ends as two pointers that only move
+// one way along a pass -- so the sort and the vote cost a few instructions per window
+// instead of a wave-wide network and per-lane searches for every window.  Phase 3: the
+// other windows (band off, > LV_CAP band elements, > CAP candidates) are re-gathered and
+// voted wave-wide (refine_window), as refine_span_kernel does.  Same results.
+constexpr int LV_W = 32;     // windows per wave
+constexpr int LV_CAP = 32;   // band elements a lane votes on
+constexpr int LV_S = 34;     // u16 per staged row (17 words: odd -> no bank conflicts)
+constexpr int LV_WMAX = 1023;   // band half-width for 16-bit offsets and prefix sums (32 * 2046 < 2^16)
+constexpr uint32_t LV_PENDING = 1u << 8, LV_U0 = 1u << 9, LV_LT = 1u << 10, LV_LE0 = 1u << 11, LV_GE0 = 1u << 12,
+                   LV_REDO = 1u << 13;
+
+struct LvMeta {
+    int32_t lo, pos;
+    uint32_t liw;     // li << 1 | w
+    uint32_t flags;   // nb | LV_* bits
+};
+
+struct LaneLds {
+    union {
+        struct {
+            uint16_t stage[LV_W * LV_S];   // staged band offsets (phase 1 -> 2)
+            union {
+                struct {
+                    int32_t cand[CAP];      // phase 1 gather
+                    int32_t ncand;
+                } g;
+                uint16_t pre[LV_W * LV_S];  // phase 2 prefix sums
+            } u;
+            LvMeta meta[LV_W];
+        } a;
+        WinLds full;                        // phase 3 (wave-wide windows)
+    };
+};
+
+template <int N>
+__device__ __forceinline__ void lane_sort(uint32_t (&x)[LV_CAP]) {   // ascending bitonic network, static indices
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; i++) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint32_t p = x[i], q = x[l];
+                    if ((i & k) == 0) { x[i] = min(p, q); x[l] = max(p, q); }
+                    else { x[i] = max(p, q); x[l] = min(p, q); }
+                }
+            }
+}
+
+// consensus_pos (refinement.c:41-101) for one lane's staged window: B[0..nb) its band's
+// sorted offsets (value - lo), P its prefix sums, w = pos - lo.  Every band value is >= 0,
+// so the reference's rounded uint64 mean of a cluster is lo + (offset sum + c/2) / c.
+__device__ __forceinline__ int32_t lane_vote(const uint16_t *B, const uint16_t *P, int32_t nb, int32_t w, int32_t lo,
+                                             uint32_t fl, const KParams &k) {
+    const int32_t ci = k.ci, range = k.range;
+    int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
+    int32_t valR = -1, maxR = k.min_count - 1, distR = 0x7fffffff;
+    // lower_bound(pos+25) over the band (refinement.c:3-10), started where the full pass would
+    int32_t uB = 0;
+    while (uB < nb && (int32_t)B[uB] <= w + SV_MIN_LENGTH / 2) uB++;
+    int32_t p = (fl & LV_U0) ? 0 : uB == 0 ? -1 : uB - 1;
+    if (nb == 0) p = -1;
+    int32_t kk = p + 1;   // first index of the cluster below i (two pointers: never moves up)
+    for (int32_t i = p; i >= 0; i--) {                                       // refinement.c:58
+        const int32_t a = B[i];
+        if (ref_abs(w - a) >= range) break;
+        kk = min(kk, i);
+        while (kk > 0 && (int32_t)B[kk - 1] >= a - ci) kk--;                 // :61
+        const int32_t c = i - kk + 1;
+        const int32_t co = (int32_t)(((uint32_t)P[i + 1] - (uint32_t)P[kk] + (uint32_t)(c / 2)) / (uint32_t)c);   // :65
+        if (c > maxL) {                                                      // :67-76
+            const int32_t d = ref_abs(w - co);
+            if (d < ci) return lo + co;
+            if (d < distL) { maxL = c; valL = lo + co; distL = d; }
+        }
+    }
+    // upper_bound(pos-25) (refinement.c:12-19): the full multiset's A[0] / A[n-1]
+    const int32_t q = (fl & LV_LT) ? ((fl & LV_LE0) ? 0 : nb) : ((fl & LV_GE0) ? nb - 1 : nb);
+    int32_t m = q + 1;    // first index past the cluster above i (never moves down)
+    for (int32_t i = q; i < nb; i++) {                                       // :80
+        const int32_t a = B[i];
+        if (ref_abs(w - a) >= range) break;
+        m = max(m, i + 1);
+        while (m < nb && (int32_t)B[m] <= a + ci) m++;                       // :83
+        const int32_t c = m - i;
+        const int32_t co = (int32_t)(((uint32_t)P[m] - (uint32_t)P[i] + (uint32_t)(c / 2)) / (uint32_t)c);
+        if (c > maxR) {                                                      // :88-97
+            const int32_t d = ref_abs(w - co);
+            if (d < ci) return lo + co;
+            if (d < distR) { maxR = c; valR = lo + co; distR = d; }
+        }
+    }
+    return distL < distR ? valL : valR;                                      // :100
+}
+
+// A2 (audit.c:176-225) for window g: kind (-1: none -> NA), s, e, pos of the vote.
+__device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &li, uint32_t &w, int32_t &chrom,
+                                         uint32_t &s, uint32_t &e, uint32_t &imp) {
+    w = g >= a.n ? 1u : 0u;
+    li = g - w * a.n;
+    const svt_locus L = a.loci[li];
+    const int32_t type = uniform_i(L.type);
+    chrom = uniform_i(L.chrom);
+    const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
+    const KParams &k = a.prm;
+    // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250): NA, NA
+    if (type == T_INS && w == 0) { s = pos - (uint32_t)k.median; e = pos + (uint32_t)k.median; imp = pos; return K_INS; }
+    if (type == T_DEL) {
+        if (w == 0) { s = pos - (uint32_t)k.wider; e = pos + (uint32_t)k.narrow; imp = pos; return K_START; }
+        s = end - (uint32_t)k.narrow; e = end + (uint32_t)k.narrow; imp = end;
+        return K_END;
+    }
+    return -1;
+}
+
+#ifndef SVT_LANE_VOTE
+#define SVT_LANE_VOTE 1
+#endif
+
+// One window's A2 + A3 answer, computed by one lane (phase 0).  u32 words only (the rows
+// it is parked in are 4-byte aligned).
+constexpr int32_t LQ_REDO = 1 << 4;   // kind bit: the window takes the wave-wide path (slow reads / e >= 2^31)
+struct LvQuery {
+    int32_t kind;          // K_* (| LQ_REDO), -1: no window (NA)
+    int32_t chrom;
+    uint32_t s, e, imp, liw;
+    uint32_t e0[2], e1[2], cb[2];   // span bounds [E0, E1), the contig's first arena offset
+};
+static_assert(sizeof(LvQuery) <= LV_S * 2, "LvQuery must fit a staging row");
+
+__device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, LvQuery &q) {
+    const DevPileup &P = a.pile;
+    const KParams &k = a.prm;
+    const uint32_t w = g >= a.n ? 1u : 0u, li = g - w * a.n;
+    const svt_locus L = a.loci[li];
+    q.kind = -1;
+    q.chrom = L.chrom;
+    q.liw = li << 1 | w;
+    const uint32_t pos = L.pos, end = L.end;
+    if (L.type == T_INS && w == 0) { q.kind = K_INS; q.s = pos - (uint32_t)k.median; q.e = pos + (uint32_t)k.median; q.imp = pos; }
+    else if (L.type == T_DEL && w == 0) { q.kind = K_START; q.s = pos - (uint32_t)k.wider; q.e = pos + (uint32_t)k.narrow; q.imp = pos; }
+    else if (L.type == T_DEL) { q.kind = K_END; q.s = end - (uint32_t)k.narrow; q.e = end + (uint32_t)k.narrow; q.imp = end; }
+    // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250): NA, NA
+    if (q.kind < 0) return;
+    if (q.e >= 0x80000000u) { q.kind |= LQ_REDO; return; }   // the exact per-read path (gather_span)
+    q.e0[0] = q.e0[1] = q.e1[0] = q.e1[1] = 0;   // empty span: no reads
+    const int tid = L.chrom - 1;
+    const int64_t beg = (int64_t)(uint32_t)(q.s - 1u), qend = (int64_t)(uint32_t)(q.e - 1u);
+    if (tid < 0 || tid >= P.n_targets || qend <= beg) return;   // A3: no reads
+    const int64_t ra = P.tid_off[tid], nr = P.tid_off[tid + 1] - ra;
+    if (nr == 0) return;
+    const int64_t b0 = P.bkt_off[tid], nb = P.bkt_off[tid + 1] - b0;   // last bucket = {nr, nr}
+    const int64_t bh = min(qend >> BKT_SHIFT, nb - 1), bl = min(beg >> BKT_SHIFT, nb - 1);
+    const uint2 h0 = P.bkt[b0 + bh], h1 = P.bkt[b0 + min(bh + 1, nb - 1)];
+    const uint2 l0 = P.bkt[b0 + bl], l1 = P.bkt[b0 + min(bl + 1, nb - 1)];
+    // hi = first read with pos >= qend in [h0.x, h1.x]; lo = first with emax > beg in [l0.y, l1.y]
+    int64_t hl = h0.x, hh = h1.x, ll = l0.y, lh = l1.y;
+    const int32_t *pp = P.pos + ra, *em = P.emax + ra;
+    while (hl < hh || ll < lh) {   // the two binary searches interleaved (their loads overlap)
+        const int64_t hm = (hl + hh) >> 1, lm = (ll + lh) >> 1;
+        const int32_t pv = hl < hh ? pp[hm] : 0, evv = ll < lh ? em[lm] : 0;
+        if (hl < hh) { if ((int64_t)pv >= qend) hh = hm; else hl = hm + 1; }
+        if (ll < lh) { if ((int64_t)evv > beg) lh = lm; else ll = lm + 1; }
+    }
+    const int64_t lo = ra + ll, hi = ra + hl;
+    if (lo >= hi) return;
+    const uint64_t *off = q.kind == K_INS ? P.spoffI : P.spoffD;
+    const uint64_t E0 = off[lo], E1 = off[hi];
+    if (P.slowpre[hi] != P.slowpre[lo]) { q.kind |= LQ_REDO; return; }   // slow reads: exact per-read replay
+    const uint64_t cb = q.kind == K_END ? P.off64[ra] : 0ull;
+    q.e0[0] = (uint32_t)E0; q.e0[1] = (uint32_t)(E0 >> 32);
+    q.e1[0] = (uint32_t)E1; q.e1[1] = (uint32_t)(E1 >> 32);
+    q.cb[0] = (uint32_t)cb; q.cb[1] = (uint32_t)(cb >> 32);
+}
+
+__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) {
+    __shared__ LaneLds lds_all[WPB];
+    const uint32_t wid = threadIdx.x >> 6;
+    const int ln = lane_id();
+    const uint32_t g0 = (blockIdx.x * WPB + wid) * LV_W, nw = 2u * a.n;
+    if (g0 >= nw) return;
+    LaneLds &L = lds_all[wid];
+    const KParams &k = a.prm;
+    const uint32_t cnt = min((uint32_t)LV_W, nw - g0);
+    const bool band_ok = k.range > SV_MIN_LENGTH / 2 && k.range + max(k.ci, 0) <= LV_WMAX && k.ci >= -LV_WMAX;
+    // ---- phase 0: every window's A2 + A3 at once, one lane each (the dependent loads of
+    // locus -> bucket words -> pos/emax searches -> span bounds run once per LV_W windows),
+    // parked in the window's staging row (read back before that row is written)
+    if ((uint32_t)ln < cnt) {
+        LvQuery q{};
+        lane_query(a, g0 + (uint32_t)ln, q);
+        *reinterpret_cast<LvQuery *>(L.a.stage + (uint32_t)ln * LV_S) = q;
+    }
+    wave_sync();
+    // ---- phase 1: span walk + band filter per window (wave-wide)
+    for (uint32_t kw = 0; kw < cnt; kw++) {
+        const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.a.stage + kw * LV_S);
+        const int32_t qk = uniform_i(qp->kind);
+        const uint32_t li = (uint32_t)uniform_i((int32_t)qp->liw) >> 1, w = (uint32_t)uniform_i((int32_t)qp->liw) & 1u;
+        const uint32_t s = (uint32_t)uniform_i((int32_t)qp->s), e = (uint32_t)uniform_i((int32_t)qp->e);
+        const uint32_t imp = (uint32_t)uniform_i((int32_t)qp->imp);
+        const int32_t chrom = uniform_i(qp->chrom);
+        const uint64_t E0 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[0]) |
+                            (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[1]) << 32;
+        const uint64_t E1 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e1[0]) |
+                            (uint64_t)(uint32_t)uniform_i((int32_t)qp->e1[1]) << 32;
+        const uint64_t cb = (uint64_t)(uint32_t)uniform_i((int32_t)qp->cb[0]) |
+                            (uint64_t)(uint32_t)uniform_i((int32_t)qp->cb[1]) << 32;
+        wave_sync();   // the row may be overwritten from here on
+        const int kind = qk & 7;
+        uint32_t flags = 0;
+        int32_t lo = 0;
+        uint32_t r = SVT_NA;
+        if (qk >= 0 && (qk & LQ_REDO)) {
+            flags = LV_REDO;
+        } else if (qk >= 0) {
+            Sink sink{L.a.u.g.cand, CAP, &L.a.u.g.ncand};
+            if (ln == 0) L.a.u.g.ncand = 0;
+            wave_sync();
+            if (E1 > E0) {
+                if (kind == K_INS) span_walk<K_INS>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink);
+                else if (kind == K_START) span_walk<K_START>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink);
+                else span_walk<K_END>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink, cb);
+            }
+            wave_sync();
+            const int32_t n = uniform_i(L.a.u.g.ncand);
+            if (n < k.min_count) {
+                r = SVT_NA;                                                   // refinement.c:43-45
+            } else if (n > CAP || !SVT_LANE_VOTE || !band_ok) {
+                flags = LV_REDO;
+            } else {
+                Band bd;
+                const int32_t nb = band_filter(L.a.u.g.cand, n, (int32_t)imp, k, bd);
+                if (!bd.on || !bd.f32 || nb > LV_CAP) {
+                    flags = LV_REDO;
+                } else {
+                    lo = bd.lo;
+                    if (ln < nb) L.a.stage[kw * LV_S + (uint32_t)ln] = (uint16_t)(L.a.u.g.cand[ln] - lo);
+                    flags = (uint32_t)nb | LV_PENDING | (bd.u == 0 ? LV_U0 : 0u) | (bd.n_lt > 0 ? LV_LT : 0u) |
+                            (bd.n_le == 0 ? LV_LE0 : 0u) | (bd.n_ge == 0 ? LV_GE0 : 0u);
+                }
+            }
+        }
+        if (ln == 0) {
+            L.a.meta[kw] = LvMeta{lo, (int32_t)imp, li << 1 | w, flags};
+            if (!(flags & (LV_PENDING | LV_REDO))) write_result(a, li, w, r);
+        }
+        wave_sync();
+    }
+    // ---- phase 2: one lane per staged window
+    uint64_t redo;   // phase 3's windows (the meta rows are overwritten by its gathers)
+    {
+        const bool mine = (uint32_t)ln < cnt;
+        const LvMeta mt = mine ? L.a.meta[ln] : LvMeta{0, 0, 0, 0};
+        const bool pend = mine && (mt.flags & LV_PENDING);
+        redo = ballot(mine && (mt.flags & LV_REDO));
+        const int32_t nb = pend ? (int32_t)(mt.flags & 0xffu) : 0;
+        const uint64_t any = ballot(pend);
+        if (any) {
+            uint32_t x[LV_CAP];
+            uint16_t *row = L.a.stage + (uint32_t)ln * LV_S;
+#pragma unroll
+            for (int j = 0; j < LV_CAP; j++) x[j] = j < nb ? (uint32_t)row[j] : 0xffffu;
+            int32_t nmax = nb;   // wave max of nb: the smallest network that sorts every lane
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
+            if (nmax <= 8) lane_sort<8>(x);
+            else if (nmax <= 16) lane_sort<16>(x);
+            else lane_sort<32>(x);
+            uint16_t *prow = L.a.u.pre + (uint32_t)ln * LV_S;
+            uint32_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < LV_CAP; j++) {
+                if (j < nb) { row[j] = (uint16_t)x[j]; prow[j] = (uint16_t)acc; acc += x[j]; }
+            }
+            if (pend) prow[nb] = (uint16_t)acc;
+            if (pend) {
+                const int32_t r = lane_vote(row, prow, nb, mt.pos - mt.lo, mt.lo, mt.flags, k);
+                write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
+            }
+        }
+        wave_sync();
+    }
+    // ---- phase 3: the windows voted wave-wide (re-gathered)
+    while (redo) {
+        const uint32_t kw = (uint32_t)__builtin_ctzll(redo);
+        redo &= redo - 1;
+        uint32_t li, w, s = 0, e = 0, imp = 0;
+        int32_t chrom;
+        const int kind = window_of(a, g0 + kw, li, w, chrom, s, e, imp);
+        unsigned long long wk[W_N];
+        int32_t sup;
+        uint32_t r;
+        if (kind == K_INS) r = (uint32_t)refine_window<K_INS, false, G_SPAN>(a, L.full, chrom, s, e, imp, wk, sup);
+        else if (kind == K_START) r = (uint32_t)refine_window<K_START, false, G_SPAN>(a, L.full, chrom, s, e, imp, wk, sup);
+        else r = (uint32_t)refine_window<K_END, false, G_SPAN>(a, L.full, chrom, s, e, imp, wk, sup);
+        if (ln == 0) write_result(a, li, w, r);
+        wave_sync();
+    }
+}
+
 // sliding_window_ins mode (sliding_window.c:8-97): one wave per sub-window.  A sub-window
 // is refine_ins's window exactly -- the same region query (sub_start-1, sub_end-1, :27),
 // the same walk (I >= 50 collects rp, advance unless I/S, break when rp > sub_end,
@@ -2110,6 +2465,7 @@ struct svt_ctx {
     svt_params prm{};
     int device = 0;
     int gather = G_SPAN;          // SVTREK_GATHER=event / index / stream / perread select the A/B variants
+    bool lane_vote = true;        // span: refine_lane_kernel; SVTREK_GATHER=span1: refine_span_kernel
     char err[512] = {0};
     // pileup
     int32_t n_targets = 0;
@@ -2277,6 +2633,9 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
     if (c->gather == G_SPAN) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_SPAN>), grid, block, 0, st, a);
+        else if (c->lane_vote)
+            hipLaunchKernelGGL(refine_lane_kernel, dim3((unsigned)((2 * n + WPB * LV_W - 1) / (WPB * LV_W))), block, 0,
+                               st, a);
         else hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
     } else if (c->gather == G_EVENT) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_EVENT>), grid, block, 0, st, a);
@@ -2479,6 +2838,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
                 : strcmp(g, "index") == 0   ? G_INDEX
                 : strcmp(g, "event") == 0   ? G_EVENT
                                             : G_SPAN;
+    c->lane_vote = !(g && strcmp(g, "span1") == 0);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;

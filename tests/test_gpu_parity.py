@@ -387,6 +387,7 @@ def test_hip_and_cpu_backends_through_one_abi(engine_factory, seed):
     with Engine(Params(), device=0, lib=cpu_lib) as cpu:
         cpu.load_pileup(pl)
         _assert_same(gpu.refine(loci), cpu.refine(loci), loci)
-        wc, wg = cpu.count_work(loci), gpu.count_work(loci)
+        nv = loci[loci["type"] != 3]   # the engine issues no INV queries (refine_point never collects)
+        wc, wg = cpu.count_work(nv), gpu.count_work(nv)
         assert (wc["windows"], wc["reads"], wc["ops_walked"], wc["candidates"]) == \
             (wg["windows"], wg["reads"], wg["ops_walked"], wg["candidates"])
