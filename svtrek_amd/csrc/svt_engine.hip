@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.10.0 (gfx950, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.10.1 (gfx950, span walk, lane vote)"
 
 namespace {
 
@@ -1966,7 +1966,10 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
 // instead of a wave-wide network and per-lane searches for every window.  Phase 3: the
 // other windows (band off, > LV_CAP band elements, > CAP candidates) are re-gathered and
 // voted wave-wide (refine_window), as refine_span_kernel does.  Same results.
-constexpr int LV_W = 32;     // windows per wave
+#ifndef SVT_LV_W
+#define SVT_LV_W 32
+#endif
+constexpr int LV_W = SVT_LV_W;   // windows per wave (<= 64: one lane each in phase 2)
 constexpr int LV_CAP = 32;   // band elements a lane votes on
 constexpr int LV_S = 34;     // u16 per staged row (17 words: odd -> no bank conflicts)
 constexpr int LV_WMAX = 1023;   // band half-width for 16-bit offsets and prefix sums (32 * 2046 < 2^16)
@@ -1982,13 +1985,12 @@ struct LvMeta {
 struct LaneLds {
     union {
         struct {
-            uint16_t stage[LV_W * LV_S];   // staged band offsets (phase 1 -> 2)
-            union {
+            uint16_t stage[LV_W * LV_S];   // parked queries (phase 0 -> 1), staged band offsets (1 -> 2)
+            struct {
                 struct {
                     int32_t cand[CAP];      // phase 1 gather
                     int32_t ncand;
                 } g;
-                uint16_t pre[LV_W * LV_S];  // phase 2 prefix sums
             } u;
             LvMeta meta[LV_W];
         } a;
@@ -2013,27 +2015,42 @@ __device__ __forceinline__ void lane_sort(uint32_t (&x)[LV_CAP]) {   // ascendin
             }
 }
 
+// floor(x / c) for x < 2^17, 1 <= c <= 64: ((x + 1/2) * rcp(c)) lies at least 1/(2c) >= 2^-7
+// inside [q, q+1) exactly, and the f32 product is within 2^-9 of it (x + 1/2 < 2^17,
+// v_rcp_f32 within 1 ulp), so the truncation is exact.
+__device__ __forceinline__ uint32_t div_small(uint32_t x, uint32_t c) {
+    return (uint32_t)(((float)x + 0.5f) * __builtin_amdgcn_rcpf((float)c));
+}
+
 // consensus_pos (refinement.c:41-101) for one lane's staged window: B[0..nb) its band's
-// sorted offsets (value - lo), P its prefix sums, w = pos - lo.  Every band value is >= 0,
-// so the reference's rounded uint64 mean of a cluster is lo + (offset sum + c/2) / c.
-__device__ __forceinline__ int32_t lane_vote(const uint16_t *B, const uint16_t *P, int32_t nb, int32_t w, int32_t lo,
-                                             uint32_t fl, const KParams &k) {
+// sorted offsets (value - lo), w = pos - lo.  Every band value is >= 0, so the reference's
+// rounded uint64 mean of a cluster is lo + (offset sum + c/2) / c.  The clusters are sliding
+// windows whose ends only move one way along each pass, so their sums are kept up to date
+// element by element (no prefix array).
+__device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int32_t w, int32_t lo, uint32_t fl,
+                                             const KParams &k) {
     const int32_t ci = k.ci, range = k.range;
     int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
     int32_t valR = -1, maxR = k.min_count - 1, distR = 0x7fffffff;
     // lower_bound(pos+25) over the band (refinement.c:3-10), started where the full pass would
-    int32_t uB = 0;
-    while (uB < nb && (int32_t)B[uB] <= w + SV_MIN_LENGTH / 2) uB++;
-    int32_t p = (fl & LV_U0) ? 0 : uB == 0 ? -1 : uB - 1;
+    int32_t l0 = 0, h0 = nb;
+    while (l0 < h0) {
+        const int32_t md = (l0 + h0) >> 1;
+        if ((int32_t)B[md] > w + SV_MIN_LENGTH / 2) h0 = md; else l0 = md + 1;
+    }
+    int32_t p = (fl & LV_U0) ? 0 : l0 == 0 ? -1 : l0 - 1;
     if (nb == 0) p = -1;
-    int32_t kk = p + 1;   // first index of the cluster below i (two pointers: never moves up)
+    int32_t kk = p + 1, prev = 0;   // cluster [kk, i] below i, its offset sum S
+    uint32_t S = 0;
     for (int32_t i = p; i >= 0; i--) {                                       // refinement.c:58
         const int32_t a = B[i];
         if (ref_abs(w - a) >= range) break;
-        kk = min(kk, i);
-        while (kk > 0 && (int32_t)B[kk - 1] >= a - ci) kk--;                 // :61
+        if (i < p) S -= (uint32_t)prev;                                      // element i+1 leaves
+        if (kk > i) { kk = i; S = (uint32_t)a; }
+        while (kk > 0 && (int32_t)B[kk - 1] >= a - ci) { kk--; S += B[kk]; }   // :61-64
+        prev = a;
         const int32_t c = i - kk + 1;
-        const int32_t co = (int32_t)(((uint32_t)P[i + 1] - (uint32_t)P[kk] + (uint32_t)(c / 2)) / (uint32_t)c);   // :65
+        const int32_t co = (int32_t)div_small(S + (uint32_t)(c / 2), (uint32_t)c);   // :65
         if (c > maxL) {                                                      // :67-76
             const int32_t d = ref_abs(w - co);
             if (d < ci) return lo + co;
@@ -2042,14 +2059,17 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, const uint16_t *
     }
     // upper_bound(pos-25) (refinement.c:12-19): the full multiset's A[0] / A[n-1]
     const int32_t q = (fl & LV_LT) ? ((fl & LV_LE0) ? 0 : nb) : ((fl & LV_GE0) ? nb - 1 : nb);
-    int32_t m = q + 1;    // first index past the cluster above i (never moves down)
+    int32_t m = q;   // cluster [i, m) above i
+    S = 0;
     for (int32_t i = q; i < nb; i++) {                                       // :80
         const int32_t a = B[i];
         if (ref_abs(w - a) >= range) break;
-        m = max(m, i + 1);
-        while (m < nb && (int32_t)B[m] <= a + ci) m++;                       // :83
+        if (i > q) S -= (uint32_t)prev;                                      // element i-1 leaves
+        if (m <= i) { m = i + 1; S = (uint32_t)a; }
+        while (m < nb && (int32_t)B[m] <= a + ci) { S += B[m]; m++; }        // :83-86
+        prev = a;
         const int32_t c = m - i;
-        const int32_t co = (int32_t)(((uint32_t)P[m] - (uint32_t)P[i] + (uint32_t)(c / 2)) / (uint32_t)c);
+        const int32_t co = (int32_t)div_small(S + (uint32_t)(c / 2), (uint32_t)c);
         if (c > maxR) {                                                      // :88-97
             const int32_t d = ref_abs(w - co);
             if (d < ci) return lo + co;
@@ -2158,6 +2178,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         *reinterpret_cast<LvQuery *>(L.a.stage + (uint32_t)ln * LV_S) = q;
     }
     wave_sync();
+    if (SVT_DIAG == 6) return;   // diagnostic build: phase 0 only
     // ---- phase 1: span walk + band filter per window (wave-wide)
     for (uint32_t kw = 0; kw < cnt; kw++) {
         const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.a.stage + kw * LV_S);
@@ -2190,7 +2211,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             }
             wave_sync();
             const int32_t n = uniform_i(L.a.u.g.ncand);
-            if (n < k.min_count) {
+            if (n < k.min_count || SVT_DIAG == 7) {
                 r = SVT_NA;                                                   // refinement.c:43-45
             } else if (n > CAP || !SVT_LANE_VOTE || !band_ok) {
                 flags = LV_REDO;
@@ -2213,6 +2234,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
+    if (SVT_DIAG == 8) return;   // diagnostic build: phases 0-1 only
     // ---- phase 2: one lane per staged window
     uint64_t redo;   // phase 3's windows (the meta rows are overwritten by its gathers)
     {
@@ -2224,30 +2246,36 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         const uint64_t any = ballot(pend);
         if (any) {
             uint32_t x[LV_CAP];
-            uint16_t *row = L.a.stage + (uint32_t)ln * LV_S;
+            // lanes without a staged window use row 0 read-only (rows exist for LV_W lanes only)
+            uint16_t *row = L.a.stage + (pend ? (uint32_t)ln : 0u) * LV_S;
+            const uint32_t *row32 = reinterpret_cast<const uint32_t *>(row);
 #pragma unroll
-            for (int j = 0; j < LV_CAP; j++) x[j] = j < nb ? (uint32_t)row[j] : 0xffffu;
+            for (int j = 0; j < LV_CAP; j += 2) {   // two offsets per 4-byte LDS read
+                const uint32_t v = row32[j >> 1];
+                x[j] = j < nb ? (v & 0xffffu) : 0xffffu;
+                x[j + 1] = j + 1 < nb ? (v >> 16) : 0xffffu;
+            }
             int32_t nmax = nb;   // wave max of nb: the smallest network that sorts every lane
 #pragma unroll
             for (int d = 32; d > 0; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
             if (nmax <= 8) lane_sort<8>(x);
             else if (nmax <= 16) lane_sort<16>(x);
             else lane_sort<32>(x);
-            uint16_t *prow = L.a.u.pre + (uint32_t)ln * LV_S;
-            uint32_t acc = 0;
-#pragma unroll
-            for (int j = 0; j < LV_CAP; j++) {
-                if (j < nb) { row[j] = (uint16_t)x[j]; prow[j] = (uint16_t)acc; acc += x[j]; }
-            }
-            if (pend) prow[nb] = (uint16_t)acc;
+            uint32_t *wrow = reinterpret_cast<uint32_t *>(row);
             if (pend) {
-                const int32_t r = lane_vote(row, prow, nb, mt.pos - mt.lo, mt.lo, mt.flags, k);
+#pragma unroll
+                for (int j = 0; j < LV_CAP; j += 2) wrow[j >> 1] = x[j] | x[j + 1] << 16;
+                const int32_t r = lane_vote(row, nb, mt.pos - mt.lo, mt.lo, mt.flags, k);
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
             }
         }
         wave_sync();
     }
     // ---- phase 3: the windows voted wave-wide (re-gathered)
+    if (SVT_DIAG == 9) {   // diagnostic build: count phase 3's windows (status word bits 8+), skip them
+        if (ln == 0 && redo) atomicAdd(a.status, (int32_t)__popcll(redo) << 8);
+        return;
+    }
     while (redo) {
         const uint32_t kw = (uint32_t)__builtin_ctzll(redo);
         redo &= redo - 1;
@@ -3146,6 +3174,11 @@ svt_status svt_sync(svt_ctx *c, void *stream) {
     if (c->have_last && c->last_stream != (hipStream_t)stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
     int32_t status = 0;
     HIP_TRY(c, hipMemcpy(&status, c->d_ctl + 8, 4, hipMemcpyDeviceToHost));
+#if SVT_DIAG == 9
+    fprintf(stderr, "[diag] wave-wide (phase 3) windows: %d\n", status >> 8);
+    HIP_TRY(c, hipMemset(c->d_ctl + 8, 0, 4));
+    status &= 1;
+#endif
     if (status & 1) {
         HIP_TRY(c, hipMemset(c->d_ctl + 8, 0, 4));   // sticky until reported
         const svt_status g = grow_pool(c);            // a re-run of the batch now fits

@@ -11,6 +11,6 @@ export TMPDIR=/tmp
 for lib in svtrek_amd/libsvtrek_hip.so svtrek_amd/diag/*.so; do
   name=$(basename "$lib" .so)
   SVTREK_ENGINE_LIB=$PWD/$lib timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
-    --output-format csv -d "$OUT/$name" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cold "$@" > "$OUT/$name.log" 2>&1 || { echo "fail $name"; tail -5 "$OUT/$name.log"; exit 1; }
+    --output-format csv -d "$OUT/$name" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cold --no-verify "$@" > "$OUT/$name.log" 2>&1 || { echo "fail $name"; tail -5 "$OUT/$name.log"; exit 1; }
   echo "done $name"
 done
