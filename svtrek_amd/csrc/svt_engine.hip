@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.10.1 (gfx950, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.10.2 (gfx950, span walk, lane vote)"
 
 namespace {
 
@@ -116,6 +116,9 @@ struct KArgs {
     uint4 *rec_out;             // gather records {index, start, end, 0} instead of `out` (or null)
     const uint32_t *rec_index;  //   index of locus i: rec_index[i], or rec_base + i when null
     uint32_t rec_base;
+    uint32_t *redo_list;        // lane-vote launches: windows left for refine_redo_kernel
+    uint32_t *redo_ctr;         //   their count (this launch's counter)
+    uint32_t *redo_next;        //   the next launch's counter (reset by refine_redo_kernel)
 };
 
 // svt_work counter slots (refine_window's wk[], the context's work words)
@@ -123,6 +126,7 @@ constexpr int W_WINDOWS = 0, W_READS = 1, W_OPS = 2, W_CANDS = 3, W_SPILLED = 4,
               W_RANGE = 7, W_LREADS = 8, W_LENTRIES = 9, W_STOPS = 10, W_STOPCH = 11, W_SQUERIES = 12,
               W_SPAN = 13, W_N = 14;
 constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status, work counters
+constexpr size_t CTL_REDO = 200;    // two redo counters (alternating launches)
 static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
 
 // ------------------------------------------------------------------ wave primitives
@@ -1994,7 +1998,7 @@ struct LaneLds {
             } u;
             LvMeta meta[LV_W];
         } a;
-        WinLds full;                        // phase 3 (wave-wide windows)
+        WinLds full;                        // scratch the span gather is handed (it uses none)
     };
 };
 
@@ -2271,24 +2275,43 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
-    // ---- phase 3: the windows voted wave-wide (re-gathered)
-    if (SVT_DIAG == 9) {   // diagnostic build: count phase 3's windows (status word bits 8+), skip them
+    // ---- the windows voted wave-wide go to refine_redo_kernel (rare: 0.6 % of cfg4's)
+    if (SVT_DIAG == 9) {   // diagnostic build: count them (status word bits 8+), nothing else
         if (ln == 0 && redo) atomicAdd(a.status, (int32_t)__popcll(redo) << 8);
         return;
     }
-    while (redo) {
-        const uint32_t kw = (uint32_t)__builtin_ctzll(redo);
-        redo &= redo - 1;
+    if (redo) {
+        uint32_t base = 0;
+        if (ln == 0) base = atomicAdd(a.redo_ctr, (uint32_t)__popcll(redo));
+        base = rdlane(base, 0);
+        if ((redo >> ln) & 1ull) a.redo_list[base + mbcnt(redo)] = g0 + (uint32_t)ln;
+    }
+}
+
+// The lane kernel's left-over windows (band off, > LV_CAP band elements, > CAP candidates,
+// slow reads, windows ending at or past 2^31), one wave each, re-gathered and voted
+// wave-wide (refine_window); the grid strides over the list.  Also resets the counter the
+// next launch will use.
+__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_redo_kernel(KArgs a) {
+    __shared__ WinLds lds_all[WPB];
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t gw = blockIdx.x * WPB + wid, nwv = gridDim.x * WPB;
+    if (gw == 0 && lane_id() == 0) *a.redo_next = 0u;
+    const uint32_t cnt = (uint32_t)uniform_i((int32_t)__hip_atomic_load(a.redo_ctr, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT));
+    WinLds &lds = lds_all[wid];
+    for (uint32_t idx = gw; idx < cnt; idx += nwv) {
+        const uint32_t g = (uint32_t)uniform_i((int32_t)a.redo_list[idx]);
         uint32_t li, w, s = 0, e = 0, imp = 0;
         int32_t chrom;
-        const int kind = window_of(a, g0 + kw, li, w, chrom, s, e, imp);
+        const int kind = window_of(a, g, li, w, chrom, s, e, imp);
         unsigned long long wk[W_N];
         int32_t sup;
-        uint32_t r;
-        if (kind == K_INS) r = (uint32_t)refine_window<K_INS, false, G_SPAN>(a, L.full, chrom, s, e, imp, wk, sup);
-        else if (kind == K_START) r = (uint32_t)refine_window<K_START, false, G_SPAN>(a, L.full, chrom, s, e, imp, wk, sup);
-        else r = (uint32_t)refine_window<K_END, false, G_SPAN>(a, L.full, chrom, s, e, imp, wk, sup);
-        if (ln == 0) write_result(a, li, w, r);
+        uint32_t r = SVT_NA;
+        if (kind == K_INS) r = (uint32_t)refine_window<K_INS, false, G_SPAN>(a, lds, chrom, s, e, imp, wk, sup);
+        else if (kind == K_START) r = (uint32_t)refine_window<K_START, false, G_SPAN>(a, lds, chrom, s, e, imp, wk, sup);
+        else if (kind == K_END) r = (uint32_t)refine_window<K_END, false, G_SPAN>(a, lds, chrom, s, e, imp, wk, sup);
+        if (lane_id() == 0) write_result(a, li, w, r);
         wave_sync();
     }
 }
@@ -2494,6 +2517,8 @@ struct svt_ctx {
     int device = 0;
     int gather = G_SPAN;          // SVTREK_GATHER=event / index / stream / perread select the A/B variants
     bool lane_vote = true;        // span: refine_lane_kernel; SVTREK_GATHER=span1: refine_span_kernel
+    uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
+    size_t redo_cap = 0;
     char err[512] = {0};
     // pileup
     int32_t n_targets = 0;
@@ -2639,6 +2664,8 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
     a.rec_out = nullptr;
     a.rec_index = nullptr;
     a.rec_base = 0;
+    a.redo_list = nullptr;
+    a.redo_ctr = a.redo_next = nullptr;
     return a;
 }
 
@@ -2652,7 +2679,10 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     // order_on); the work counters of a counting launch start from zero; the head word is
     // cleared once per epoch cycle
     c->epoch = c->epoch % ((1u << 24) - 1u) + 1u;
-    if (c->epoch == 1) HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 8, st));
+    if (c->epoch == 1) {   // a new epoch cycle: pool head and both redo counters start from zero
+        HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 8, st));
+        HIP_TRY(c, hipMemsetAsync(c->d_ctl + CTL_REDO, 0, 8, st));
+    }
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_ctl + 16, 0, 8 * W_N, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
     a.rec_out = reinterpret_cast<uint4 *>(rec_out);
@@ -2661,9 +2691,20 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
     if (c->gather == G_SPAN) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_SPAN>), grid, block, 0, st, a);
-        else if (c->lane_vote)
+        else if (c->lane_vote) {
+            if (c->redo_cap < 2 * n) {   // window list of the wave-wide left-overs (grown, never shrunk)
+                hfree(c->d_redo);
+                c->redo_cap = 0;
+                HIP_TRY(c, hipMalloc(&c->d_redo, 2 * n * sizeof(uint32_t)));
+                c->redo_cap = 2 * n;
+            }
+            a.redo_list = c->d_redo;
+            a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->epoch & 1u);
+            a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + ((c->epoch + 1u) & 1u);
             hipLaunchKernelGGL(refine_lane_kernel, dim3((unsigned)((2 * n + WPB * LV_W - 1) / (WPB * LV_W))), block, 0,
                                st, a);
+            hipLaunchKernelGGL(refine_redo_kernel, dim3(1024), block, 0, st, a);
+        }
         else hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
     } else if (c->gather == G_EVENT) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_EVENT>), grid, block, 0, st, a);
@@ -3413,7 +3454,7 @@ void svt_close(svt_ctx *c) {
     DevGuard dg(c->device);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     free_pileup(c);
-    hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->poa_small.d); hfree(c->poa_big.d);
+    hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->d_redo); hfree(c->poa_small.d); hfree(c->poa_big.d);
     delete c;
 }
 
