@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.10.2 (gfx950, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.10.4 (gfx950, span walk, lane vote)"
 
 namespace {
 
@@ -1529,6 +1529,50 @@ __device__ __forceinline__ int32_t band_filter(int32_t *buf, int32_t n, int32_t 
     return cnt;
 }
 
+// band_filter for any n (the spill slab, > 4*WAVE candidates): the same counts and the same
+// in-place compaction, 64 elements per step (writes never pass the block being read).
+__device__ __forceinline__ int32_t band_filter_large(int32_t *buf, int32_t n, int32_t pos, const KParams &k,
+                                                     Band &bd) {
+    constexpr int32_t LIM = 1 << 30, WMAX = 1 << 22;
+    if (k.range <= SV_MIN_LENGTH / 2 || pos <= -LIM || pos >= LIM || k.range > WMAX || k.ci > WMAX - k.range ||
+        k.ci < -WMAX)
+        return n;
+    const int ln = lane_id();
+    const int32_t w = k.range + max(k.ci, 0);
+    const int32_t lo = pos - w, hi = pos + w;
+    int32_t u = 0, nlt = 0, nle = 0, nge = 0;
+    uint64_t bad = 0, neg = 0;
+    for (int32_t b = 0; b < n; b += WAVE) {
+        const int32_t i = b + ln;
+        const bool v = i < n;
+        const int32_t x = v ? buf[i] : 0;
+        u += __popcll(ballot(v && x <= pos + SV_MIN_LENGTH / 2));
+        nlt += __popcll(ballot(v && x < pos - SV_MIN_LENGTH / 2));
+        nle += __popcll(ballot(v && x <= lo));
+        nge += __popcll(ballot(v && x >= hi));
+        bad |= ballot(v && (x <= -LIM || x >= LIM));
+        neg |= ballot(v && lo < x && x < hi && x < 0);
+    }
+    if (bad) return n;
+    bd.on = true;
+    bd.f32 = neg == 0;
+    bd.u = u; bd.n_lt = nlt; bd.n_le = nle; bd.n_ge = nge;
+    bd.lo = lo; bd.hi = hi;
+    wave_sync();
+    int32_t cnt = 0;
+    for (int32_t b = 0; b < n; b += WAVE) {
+        const int32_t i = b + ln;
+        const int32_t x = i < n ? buf[i] : 0;
+        const bool keep = i < n && lo < x && x < hi;
+        const uint64_t m = ballot(keep);
+        wave_sync();
+        if (keep) buf[cnt + (int32_t)mbcnt(m)] = x;
+        cnt += (int32_t)__popcll(m);
+        wave_sync();
+    }
+    return cnt;
+}
+
 __device__ __forceinline__ int32_t first_greater32(const int32_t *buf, int32_t l, int32_t h, int32_t key) {
     while (l < h) {
         int32_t m = (l + h) >> 1;
@@ -1679,10 +1723,11 @@ constexpr int V_CONSENSUS = 0, V_SLIDING = 1;
 // LARGE: n > 4*WAVE is known (the spill slab): only the global bitonic + the int64 vote.
 template <int VOTE, bool LARGE = false>
 __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32_t n, int32_t pos, const KParams &k,
-                                                 int32_t &support) {
+                                                 int32_t &support, const Band *given = nullptr) {
     const int ln = lane_id();
     Band bd;
-    if (!LARGE && VOTE == V_CONSENSUS && SVT_BAND && n <= 4 * WAVE) n = band_filter(buf, n, pos, k, bd);
+    if (given) bd = *given;   // buf already holds the band (band_filter_large)
+    else if (!LARGE && VOTE == V_CONSENSUS && SVT_BAND && n <= 4 * WAVE) n = band_filter(buf, n, pos, k, bd);
     int32_t x0 = 0;   // sorted element ln, from the register sorts (no LDS read-back below)
     if (LARGE) {
         int N = 1;
@@ -1812,6 +1857,16 @@ __device__ __forceinline__ int32_t vote_window(const KArgs &a, WinLds &lds, int 
     WinStats st2;
     Sink s2{g, N, &lds.ncand};
     gather<KIND, false, G>(a, chrom - 1, s, e, s2, st2, lds);
+    if (VOTE == V_CONSENSUS && SVT_BAND) {   // the exact band first: usually small enough for the register sort
+        Band bd;
+        const int32_t nb = band_filter_large(g, n, (int32_t)imprecise, a.prm, bd);
+        if (bd.on && nb <= CAP) {
+            for (int32_t i = lane_id(); i < nb; i += WAVE) lds.cand[i] = g[i];
+            wave_sync();
+            return sort_and_vote<VOTE>(lds.cand, lds.pre, nb, (int32_t)imprecise, a.prm, support, &bd);
+        }
+        if (bd.on) return sort_and_vote<VOTE, true>(g, gp, nb, (int32_t)imprecise, a.prm, support, &bd);
+    }
     return sort_and_vote<VOTE, true>(g, gp, n, (int32_t)imprecise, a.prm, support);
 }
 
@@ -2703,7 +2758,7 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
             a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + ((c->epoch + 1u) & 1u);
             hipLaunchKernelGGL(refine_lane_kernel, dim3((unsigned)((2 * n + WPB * LV_W - 1) / (WPB * LV_W))), block, 0,
                                st, a);
-            hipLaunchKernelGGL(refine_redo_kernel, dim3(1024), block, 0, st, a);
+            hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
         }
         else hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
     } else if (c->gather == G_EVENT) {
