@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.10.4 (gfx950, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.10.5 (gfx950, span walk, lane vote)"
 
 namespace {
 
@@ -1228,10 +1228,22 @@ __device__ __forceinline__ bool span_query(const DevPileup &P, int tid, int64_t 
 // The span walk proper: events [E0, E1) of the yielded reads [lo, hi) of window [s, e]
 // (query beg = s-1), nslow = the slow reads among them.  Leaves the candidate count in
 // *sink.cnt.
+// A refine_end stop search deferred by the lane kernel: the breaking read's arena offset / 32,
+// its pos, the window end, the window (searched later for a whole chunk of windows at once).
+struct StopReq {
+    uint32_t op32, rpos, e, kw;
+};
+struct StopList {
+    StopReq *q;
+    int32_t *cnt;   // LDS counter (may exceed cap: the window then takes the wave-wide path)
+    int32_t cap;
+    uint32_t kw;
+};
+
 template <int KIND>
 __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t s, uint32_t e, int64_t lo, int64_t hi,
                                           uint64_t E0, uint64_t E1, uint64_t nslow, Sink &sink,
-                                          uint64_t cbase_in = ~0ull) {
+                                          uint64_t cbase_in = ~0ull, const StopList *defer = nullptr) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u);
     const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);   // read_range yielded reads: beg < end <= 2^31 - 1
     const int ln = lane_id();
@@ -1274,7 +1286,16 @@ __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t 
             cnt += (int32_t)__popcll(m);
             if (KIND == K_END && SVT_DIAG != 3) {
                 uint64_t sm = ballot(brk);
-                if (sm) {   // the position after the break op, rare: the sink's LDS counter takes over
+                if (sm && defer) {   // queued: the lane kernel searches a whole chunk's reads at once
+                    int32_t base = 0;
+                    if (ln == 0) base = atomicAdd(defer->cnt, (int32_t)__popcll(sm));
+                    base = rdlane_i(base, 0);
+                    const int32_t qi = base + (int32_t)mbcnt(sm);
+                    if (brk && qi < defer->cap) {
+                        const uint64_t op0 = cbase + (uint64_t)(v[u].w - (uint32_t)cbase);
+                        defer->q[qi] = StopReq{(uint32_t)(op0 / ALIGN_OPS), x, e, defer->kw};
+                    }
+                } else if (sm) {   // the position after the break op, rare: the sink's LDS counter takes over
                     if (ln == 0) *sink.cnt = cnt;
                     wave_sync();
                     while (sm) sm = stop_rows(P, cbase, sm, NCIG_MASK, x, v[u].w, e, sink);
@@ -2039,7 +2060,10 @@ struct LvMeta {
     int32_t lo, pos;
     uint32_t liw;     // li << 1 | w
     uint32_t flags;   // nb | LV_* bits
+    int32_t n;        // candidates (min_count test)
 };
+constexpr int LV_STOPS = 64;   // deferred stop searches per chunk
+constexpr uint32_t LV_NONE = 1u << 14;   // no window (INV / other types): NA
 
 struct LaneLds {
     union {
@@ -2052,6 +2076,8 @@ struct LaneLds {
                 } g;
             } u;
             LvMeta meta[LV_W];
+            StopReq stops[LV_STOPS];
+            int32_t nstops;
         } a;
         WinLds full;                        // scratch the span gather is handed (it uses none)
     };
@@ -2162,6 +2188,40 @@ __device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &l
 #define SVT_LANE_VOTE 1
 #endif
 
+// One deferred stop search, per lane (refinement.c:210-221 for a read that breaks): the
+// position after the op whose walk end first passes e.  The chunk index holds the walk
+// position after every 8 arena ops; the read's chunks are scanned 4 at a time (its first
+// chunk is 4-chunk aligned: reads start on 32-op boundaries), then the break chunk's 8 ops.
+__device__ __forceinline__ uint32_t stop_lane(const DevPileup &P, const StopReq &r) {
+    const uint64_t op0 = (uint64_t)r.op32 * ALIGN_OPS, c0 = op0 / CHUNK;
+    uint32_t prev = r.rpos, bc = 0, before = r.rpos;
+    for (uint32_t c = 0;; c += 4) {   // the break exists (walk end > e): the scan ends inside the read
+        const uint4 q = *reinterpret_cast<const uint4 *>(P.chunk + c0 + c);
+        const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
+        int f = 4;
+#pragma unroll
+        for (int i = 3; i >= 0; i--)
+            if (E[i] > r.e) f = i;
+        if (f < 4) {
+            bc = c + (uint32_t)f;
+            before = f == 0 ? prev : E[f - 1];
+            break;
+        }
+        prev = E[3];
+    }
+    const uint4 *cw = reinterpret_cast<const uint4 *>(P.cigar + op0 + (uint64_t)bc * CHUNK);
+    const uint4 w0 = cw[0], w1 = cw[1];
+    const uint32_t W[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    uint32_t after = before, res = 0;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        after += ref_adv(W[i]);
+        if (!found && after > r.e) { res = after; found = true; }
+    }
+    return res + 1u;   // refinement.c:220
+}
+
 // One window's A2 + A3 answer, computed by one lane (phase 0).  u32 words only (the rows
 // it is parked in are 4-byte aligned).
 constexpr int32_t LQ_REDO = 1 << 4;   // kind bit: the window takes the wave-wide path (slow reads / e >= 2^31)
@@ -2236,6 +2296,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         lane_query(a, g0 + (uint32_t)ln, q);
         *reinterpret_cast<LvQuery *>(L.a.stage + (uint32_t)ln * LV_S) = q;
     }
+    if (ln == 0) L.a.nstops = 0;
     wave_sync();
     if (SVT_DIAG == 6) return;   // diagnostic build: phase 0 only
     // ---- phase 1: span walk + band filter per window (wave-wide)
@@ -2255,24 +2316,26 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         wave_sync();   // the row may be overwritten from here on
         const int kind = qk & 7;
         uint32_t flags = 0;
-        int32_t lo = 0;
-        uint32_t r = SVT_NA;
-        if (qk >= 0 && (qk & LQ_REDO)) {
+        int32_t lo = 0, n = 0;
+        if (qk < 0) {
+            flags = LV_NONE;
+        } else if (qk & LQ_REDO) {
             flags = LV_REDO;
-        } else if (qk >= 0) {
+        } else {
             Sink sink{L.a.u.g.cand, CAP, &L.a.u.g.ncand};
+            const StopList defer{L.a.stops, &L.a.nstops, LV_STOPS, kw};
+            const int32_t ns0 = uniform_i(L.a.nstops);
             if (ln == 0) L.a.u.g.ncand = 0;
             wave_sync();
             if (E1 > E0) {
                 if (kind == K_INS) span_walk<K_INS>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink);
                 else if (kind == K_START) span_walk<K_START>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink);
-                else span_walk<K_END>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink, cb);
+                else span_walk<K_END>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink, cb, &defer);
             }
             wave_sync();
-            const int32_t n = uniform_i(L.a.u.g.ncand);
-            if (n < k.min_count || SVT_DIAG == 7) {
-                r = SVT_NA;                                                   // refinement.c:43-45
-            } else if (n > CAP || !SVT_LANE_VOTE || !band_ok) {
+            n = uniform_i(L.a.u.g.ncand);
+            const int32_t ns1 = uniform_i(L.a.nstops);
+            if (n > CAP || !SVT_LANE_VOTE || !band_ok || ns1 > LV_STOPS || SVT_DIAG == 7) {
                 flags = LV_REDO;
             } else {
                 Band bd;
@@ -2286,10 +2349,37 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                             (bd.n_le == 0 ? LV_LE0 : 0u) | (bd.n_ge == 0 ? LV_GE0 : 0u);
                 }
             }
+            n += ns1 - ns0;   // the deferred stop candidates count toward min_count
         }
-        if (ln == 0) {
-            L.a.meta[kw] = LvMeta{lo, (int32_t)imp, li << 1 | w, flags};
-            if (!(flags & (LV_PENDING | LV_REDO))) write_result(a, li, w, r);
+        if (ln == 0) L.a.meta[kw] = LvMeta{lo, (int32_t)imp, li << 1 | w, flags, n};
+        wave_sync();
+    }
+    // ---- phase 1b: the chunk's deferred stop searches, one lane each, folded into their
+    // windows' bands (counts by LDS atomics; band members appended to the staging rows)
+    {
+        const int32_t nsq = min(uniform_i(L.a.nstops), LV_STOPS);
+        if (ln < nsq) {
+            const StopReq rq = L.a.stops[ln];
+            const int32_t v = (int32_t)stop_lane(a.pile, rq);
+            LvMeta &m = L.a.meta[rq.kw];
+            const uint32_t fl = m.flags;
+            if (fl & LV_PENDING) {
+                constexpr int32_t LIM = 1 << 30;
+                const int32_t pos = m.pos, lo = m.lo, hi = lo + 2 * (k.range + max(k.ci, 0));
+                uint32_t clr = 0, set = 0;
+                if (v <= pos + SV_MIN_LENGTH / 2) clr |= LV_U0;
+                if (v < pos - SV_MIN_LENGTH / 2) set |= LV_LT;
+                if (v <= lo) clr |= LV_LE0;
+                if (v >= hi) clr |= LV_GE0;
+                if (v <= -LIM || v >= LIM || (lo < v && v < hi && v < 0)) set |= LV_REDO;
+                if (clr) atomicAnd(&m.flags, ~clr);
+                if (set) atomicOr(&m.flags, set);
+                if (lo < v && v < hi) {
+                    const uint32_t idx = atomicAdd(&m.flags, 1u) & 0xffu;   // nb is the low byte
+                    if (idx < (uint32_t)LV_CAP) L.a.stage[rq.kw * LV_S + idx] = (uint16_t)(v - lo);
+                    else atomicOr(&m.flags, LV_REDO);
+                }
+            }
         }
         wave_sync();
     }
@@ -2298,9 +2388,13 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     uint64_t redo;   // phase 3's windows (the meta rows are overwritten by its gathers)
     {
         const bool mine = (uint32_t)ln < cnt;
-        const LvMeta mt = mine ? L.a.meta[ln] : LvMeta{0, 0, 0, 0};
-        const bool pend = mine && (mt.flags & LV_PENDING);
-        redo = ballot(mine && (mt.flags & LV_REDO));
+        const LvMeta mt = mine ? L.a.meta[ln] : LvMeta{0, 0, 0, 0, 0};
+        // decisions: no window or fewer than min_count candidates -> NA (refinement.c:43-45);
+        // the wave-wide path; or this lane's vote
+        const bool na = mine && ((mt.flags & LV_NONE) || (!(mt.flags & LV_REDO) && mt.n < k.min_count));
+        if (na) write_result(a, mt.liw >> 1, mt.liw & 1u, SVT_NA);
+        redo = ballot(mine && !na && (mt.flags & LV_REDO));
+        const bool pend = mine && !na && !(mt.flags & LV_REDO) && (mt.flags & LV_PENDING);
         const int32_t nb = pend ? (int32_t)(mt.flags & 0xffu) : 0;
         const uint64_t any = ballot(pend);
         if (any) {
