@@ -391,3 +391,37 @@ def test_hip_and_cpu_backends_through_one_abi(engine_factory, seed):
         wc, wg = cpu.count_work(nv), gpu.count_work(nv)
         assert (wc["windows"], wc["reads"], wc["ops_walked"], wc["candidates"]) == \
             (wg["windows"], wg["reads"], wg["ops_walked"], wg["candidates"])
+
+
+@pytest.mark.parametrize("nsplit", [20, 90, 300])
+def test_lane_kernel_stop_queue_and_left_overs(engine_factory, nsplit):
+    """refine_lane_kernel's deferred refine_end stop searches: many split reads (leading S,
+    walk past the window end) at DEL ends -- a chunk's queue of 64 overflows at 90+ (the
+    windows go to refine_redo_kernel) -- next to windows whose bands exceed 32 members and a
+    window with > 256 candidates (spill slab), all against the oracle."""
+    from svtrek_amd.pileup import from_reads
+    rng = np.random.default_rng(nsplit)
+    rows, loci = [], []
+    for k in range(40):
+        c = 50000 + k * 30000
+        end = c + 3000
+        loci.append((2, 1, c, end))
+        for _ in range(int(rng.integers(0, 12))):   # DEL-start support
+            p0 = c - int(rng.integers(500, 4000))
+            rows.append((0, p0, [(0, c - p0 + int(rng.integers(-6, 7))), (2, 3000), (0, 2000)]))
+        for _ in range(nsplit // 10 if k % 3 else nsplit):   # split reads at the DEL end: S, then a long M
+            p0 = end + int(rng.integers(-1900, 1900))
+            rows.append((0, p0, [(4, 500), (0, int(rng.integers(1, 40))), (1, 60), (0, 6000)]))
+        if k == 7:   # a dense band: 60 candidates within a few bp of pos
+            for _ in range(60):
+                p0 = c - 1000
+                rows.append((0, p0, [(0, 1000 + int(rng.integers(-3, 4))), (2, 3000), (0, 500)]))
+        if k == 11:  # > 256 candidates in one window
+            for _ in range(300):
+                p0 = c - int(rng.integers(2000, 15000))
+                rows.append((0, p0, [(0, c - p0 + int(rng.integers(-400, 400))), (2, 80), (0, 300)]))
+    pl = from_reads(1, rows, clip=None)
+    eng = engine_factory()
+    eng.load_pileup(pl)
+    lc = make_loci(loci)
+    _assert_same(eng.refine(lc), O.refine_batch(pl, lc), lc)
