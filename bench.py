@@ -287,6 +287,8 @@ def main() -> int:
     gather_variant = os.environ.get("SVTREK_GATHER", "span")
     kernel = {"span": "refine_lane_kernel", "span1": "refine_span_kernel", "event": "refine_event_kernel",
               "index": "refine_index_kernel"}.get(gather_variant, "refine_kernel")
+    if kernel == "refine_lane_kernel" and not os.environ.get("SVTREK_LANE_W") and 2 * n < 65536:
+        kernel = "refine_span_kernel"   # the engine's size-based pick (svt_engine.hip, launch)
     traffic, traffic_src = _traffic(args.workload, kernel, records=True)
     if args.scale != 1.0 or world > 1:
         traffic = traffic_src = None

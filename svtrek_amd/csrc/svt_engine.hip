@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.10.5 (gfx950, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.10.6 (gfx950, span walk, lane vote)"
 
 namespace {
 
@@ -2046,10 +2046,8 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
 // instead of a wave-wide network and per-lane searches for every window.  Phase 3: the
 // other windows (band off, > LV_CAP band elements, > CAP candidates) are re-gathered and
 // voted wave-wide (refine_window), as refine_span_kernel does.  Same results.
-#ifndef SVT_LV_W
-#define SVT_LV_W 32
-#endif
-constexpr int LV_W = SVT_LV_W;   // windows per wave (<= 64: one lane each in phase 2)
+// windows per wave (<= 64: one lane each in phase 2): 32, or 8 for batches too small to fill
+// the chip with 32 per wave (svt_ctx::launch)
 constexpr int LV_CAP = 32;   // band elements a lane votes on
 constexpr int LV_S = 34;     // u16 per staged row (17 words: odd -> no bank conflicts)
 constexpr int LV_WMAX = 1023;   // band half-width for 16-bit offsets and prefix sums (32 * 2046 < 2^16)
@@ -2065,17 +2063,18 @@ struct LvMeta {
 constexpr int LV_STOPS = 64;   // deferred stop searches per chunk
 constexpr uint32_t LV_NONE = 1u << 14;   // no window (INV / other types): NA
 
+template <int W>
 struct LaneLds {
     union {
         struct {
-            uint16_t stage[LV_W * LV_S];   // parked queries (phase 0 -> 1), staged band offsets (1 -> 2)
+            uint16_t stage[W * LV_S];      // parked queries (phase 0 -> 1), staged band offsets (1 -> 2)
             struct {
                 struct {
                     int32_t cand[CAP];      // phase 1 gather
                     int32_t ncand;
                 } g;
             } u;
-            LvMeta meta[LV_W];
+            LvMeta meta[W];
             StopReq stops[LV_STOPS];
             int32_t nstops;
         } a;
@@ -2278,13 +2277,14 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, LvQuery &
     q.cb[0] = (uint32_t)cb; q.cb[1] = (uint32_t)(cb >> 32);
 }
 
+template <int LV_W>
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) {
-    __shared__ LaneLds lds_all[WPB];
+    __shared__ LaneLds<LV_W> lds_all[WPB];
     const uint32_t wid = threadIdx.x >> 6;
     const int ln = lane_id();
     const uint32_t g0 = (blockIdx.x * WPB + wid) * LV_W, nw = 2u * a.n;
     if (g0 >= nw) return;
-    LaneLds &L = lds_all[wid];
+    LaneLds<LV_W> &L = lds_all[wid];
     const KParams &k = a.prm;
     const uint32_t cnt = min((uint32_t)LV_W, nw - g0);
     const bool band_ok = k.range > SV_MIN_LENGTH / 2 && k.range + max(k.ci, 0) <= LV_WMAX && k.ci >= -LV_WMAX;
@@ -2666,6 +2666,7 @@ struct svt_ctx {
     int device = 0;
     int gather = G_SPAN;          // SVTREK_GATHER=event / index / stream / perread select the A/B variants
     bool lane_vote = true;        // span: refine_lane_kernel; SVTREK_GATHER=span1: refine_span_kernel
+    int lane_w = 0;               // SVTREK_LANE_W=8|32 forces the lane kernel's windows per wave (A/B)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
     char err[512] = {0};
@@ -2840,7 +2841,11 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
     if (c->gather == G_SPAN) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_SPAN>), grid, block, 0, st, a);
-        else if (c->lane_vote) {
+        // lane kernel (32 windows a wave) once the batch has >= 64K windows; below that the
+        // one-wave-per-window span kernel is as fast or faster (fewer, longer waves leave the
+        // chip underfilled: cfg2 20K windows 33 us span vs 76 us lane<8>, 107 us lane<32>;
+        // cfg3 100K windows 111 vs 109 us; cfg4 2M windows 2.23 ms vs 0.905 ms)
+        else if (c->lane_vote && (c->lane_w != 0 || 2 * n >= (size_t)65536)) {
             if (c->redo_cap < 2 * n) {   // window list of the wave-wide left-overs (grown, never shrunk)
                 hfree(c->d_redo);
                 c->redo_cap = 0;
@@ -2850,11 +2855,19 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
             a.redo_list = c->d_redo;
             a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->epoch & 1u);
             a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + ((c->epoch + 1u) & 1u);
-            hipLaunchKernelGGL(refine_lane_kernel, dim3((unsigned)((2 * n + WPB * LV_W - 1) / (WPB * LV_W))), block, 0,
-                               st, a);
+            if (c->lane_w == 8)
+                hipLaunchKernelGGL(refine_lane_kernel<8>, dim3((unsigned)((2 * n + WPB * 8 - 1) / (WPB * 8))), block, 0,
+                                   st, a);
+            else
+                hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
+                                   st, a);
             hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
+        } else {
+            // the redo kernel of a lane launch zeroes the next epoch's counter; without one, do it here
+            if (c->lane_vote)
+                HIP_TRY(c, hipMemsetAsync(c->d_ctl + CTL_REDO + 4u * ((c->epoch + 1u) & 1u), 0, 4, st));
+            hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
         }
-        else hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
     } else if (c->gather == G_EVENT) {
         if (count) hipLaunchKernelGGL((refine_kernel<true, G_EVENT>), grid, block, 0, st, a);
         else hipLaunchKernelGGL(refine_event_kernel, grid, block, 0, st, a);
@@ -3057,6 +3070,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
                 : strcmp(g, "event") == 0   ? G_EVENT
                                             : G_SPAN;
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
+    if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;

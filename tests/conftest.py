@@ -28,18 +28,29 @@ def engine_factory():
 
     engines = []
 
+    # gather variant -> (SVTREK_GATHER, SVTREK_LANE_W)
+    variants = {"span": ("span", "32"), "lane8": ("span", "8"), "auto": ("span", None), "span1": ("span1", None)}
+
     def make(params=None, gather="span"):
-        """gather: "span" (span events, default), "event" (candidate-op lists), "index" (chunk-index walk),
-        "stream" (full CIGAR stream) or "perread" (per-read walk) -- the SVTREK_GATHER variants of the engine."""
-        old = os.environ.get("SVTREK_GATHER")
-        os.environ["SVTREK_GATHER"] = gather
+        """gather: "span" (span events through refine_lane_kernel<32> at every batch size -- the
+        product picks it from 64K windows up), "lane8" (refine_lane_kernel<8>), "span1" (one wave per
+        window, refine_span_kernel: the product's pick for smaller batches), "auto" (the product's
+        size-based pick), "event" (candidate-op lists), "index" (chunk-index walk), "stream" (full
+        CIGAR stream) or "perread" (per-read walk) -- the SVTREK_GATHER variants of the engine."""
+        g, lw = variants.get(gather, (gather, None))
+        old = {k: os.environ.get(k) for k in ("SVTREK_GATHER", "SVTREK_LANE_W")}
+        os.environ["SVTREK_GATHER"] = g
+        os.environ.pop("SVTREK_LANE_W", None)
+        if lw:
+            os.environ["SVTREK_LANE_W"] = lw
         try:
             e = Engine(params or Params(), device=0)
         finally:
-            if old is None:
-                os.environ.pop("SVTREK_GATHER", None)
-            else:
-                os.environ["SVTREK_GATHER"] = old
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         engines.append(e)
         return e
 

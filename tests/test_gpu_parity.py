@@ -38,12 +38,13 @@ def test_consensus_vectors_through_kernel(engine_factory):
         assert int(O.refine_batch(pl, loci)["start"][0]) == exp
 
 
+@pytest.mark.parametrize("gather", ["span", "lane8", "span1"])
 @pytest.mark.parametrize("seed", range(6))
-def test_random_consensus_windows(engine_factory, seed):
+def test_random_consensus_windows(engine_factory, seed, gather):
     rng = np.random.default_rng(seed)
     eng = engine_factory(Params(consensus_interval=int(rng.choice([0, 1, 5, 12])),
                                 consensus_interval_range=int(rng.choice([50, 500, 900])),
-                                consensus_min_count=int(rng.choice([1, 2, 3, 5]))))
+                                consensus_min_count=int(rng.choice([1, 2, 3, 5]))), gather=gather)
     base = 200000
     rows, vals = [], []
     for k in range(40):
@@ -61,7 +62,7 @@ def test_random_consensus_windows(engine_factory, seed):
     _assert_same(got, want, loci)
 
 
-@pytest.mark.parametrize("gather", ["span", "event", "index", "stream", "perread"])
+@pytest.mark.parametrize("gather", ["span", "lane8", "span1", "event", "index", "stream", "perread"])
 @pytest.mark.parametrize("seed", range(10))
 def test_fuzz_pileups(engine_factory, seed, gather):
     rng = np.random.default_rng(1000 + seed)
@@ -393,8 +394,9 @@ def test_hip_and_cpu_backends_through_one_abi(engine_factory, seed):
             (wg["windows"], wg["reads"], wg["ops_walked"], wg["candidates"])
 
 
+@pytest.mark.parametrize("gather", ["span", "lane8"])
 @pytest.mark.parametrize("nsplit", [20, 90, 300])
-def test_lane_kernel_stop_queue_and_left_overs(engine_factory, nsplit):
+def test_lane_kernel_stop_queue_and_left_overs(engine_factory, nsplit, gather):
     """refine_lane_kernel's deferred refine_end stop searches: many split reads (leading S,
     walk past the window end) at DEL ends -- a chunk's queue of 64 overflows at 90+ (the
     windows go to refine_redo_kernel) -- next to windows whose bands exceed 32 members and a
@@ -421,7 +423,39 @@ def test_lane_kernel_stop_queue_and_left_overs(engine_factory, nsplit):
                 p0 = c - int(rng.integers(2000, 15000))
                 rows.append((0, p0, [(0, c - p0 + int(rng.integers(-400, 400))), (2, 80), (0, 300)]))
     pl = from_reads(1, rows, clip=None)
-    eng = engine_factory()
+    eng = engine_factory(gather=gather)
     eng.load_pileup(pl)
     lc = make_loci(loci)
     _assert_same(eng.refine(lc), O.refine_batch(pl, lc), lc)
+
+
+def test_size_based_kernel_pick_alternating(engine_factory):
+    """The product's own pick: batches below 64K windows run refine_span_kernel, larger ones
+    refine_lane_kernel<32> + refine_redo_kernel, whose left-over counters alternate by launch;
+    interleaving small and large batches on one context (and a device-side stream of launches
+    without host syncs between them) must keep every result equal to the oracle's."""
+    import torch
+    rng = np.random.default_rng(77)
+    hot = [int(x) for x in rng.integers(5000, 55000, size=8)]
+    pl = random_pileup(rng, n_targets=2, contig_len=60000, n_reads=600, max_ops=150, hot=hot)
+    eng = engine_factory(gather="auto")
+    eng.load_pileup(pl)
+    big = random_loci(rng, 40000, 2, 60000, hot)     # 80K windows: lane kernel
+    small = random_loci(rng, 3000, 2, 60000, hot)    # 6K windows: span kernel
+    want_b, want_s = O.refine_batch(pl, big), O.refine_batch(pl, small)
+    for batch, want in ((big, want_b), (small, want_s), (big, want_b), (big, want_b), (small, want_s),
+                        (small, want_s), (big, want_b)):
+        _assert_same(eng.refine(batch), want, batch)
+    # the same sequence queued on one stream, checked after a single sync
+    from svtrek_amd._lib import LOCUS_DTYPE, RESULT_DTYPE
+    seq = [big, small, small, big, small, big, big]
+    dev = [torch.from_numpy(np.ascontiguousarray(b, dtype=LOCUS_DTYPE).view(np.uint8)).cuda() for b in seq]
+    outs = [torch.empty(len(b) * RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for b in seq]
+    s = torch.cuda.current_stream().cuda_stream
+    for b, d, o in zip(seq, dev, outs):
+        eng.refine_device(d.data_ptr(), len(b), o.data_ptr(), s)
+    eng.sync(s)
+    torch.cuda.synchronize()
+    for b, o in zip(seq, outs):
+        got = o.cpu().numpy().view(RESULT_DTYPE)
+        _assert_same(got, want_b if b is big else want_s, b)

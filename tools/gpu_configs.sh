@@ -1,6 +1,7 @@
 #!/bin/bash
-# Run ON THE GPU BOX: the headline bench (cfg2, with CPU baseline) and the other BASELINE
-# workloads (kernel throughput only).  Each step has its own time limit; stops at the first failure.
+# Run ON THE GPU BOX: kernel throughput on the other BASELINE workloads (the headline cfg4 line
+# is bench.py's default).  Each step has its own time limit; stops at the first failure.
+#   tools/gpu_configs.sh TAG
 set -u
 TAG=${1:?tag}
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -15,7 +16,7 @@ run() {  # name, timeout, args...
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
   tail -1 "$OUT/$name.log"
 }
-[ "${SKIP_CFG2:-0}" = 1 ] || run cfg2 400 --steps 20 --warmup 3
-run cfg4 400 --workload cfg4_1m_delins_30x_hifi --steps 10 --warmup 2 --no-cpu-baseline
-run cfg3 600 --workload cfg3_50k_delins_30x_ont --steps 10 --warmup 2 --no-cpu-baseline
-#run cfg5q 900 --workload cfg5_100k_60x_ul_ont --scale 0.25 --steps 10 --warmup 2 --no-cpu-baseline
+run cfg2 300 --workload cfg2_10kdel_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
+run cfg3 300 --workload cfg3_50k_delins_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
+run cfg1 200 --workload cfg1_100del_10x --steps 20 --warmup 3 --no-cpu-baseline
+run cfg5q 600 --workload cfg5_100k_60x_ul_ont --scale 0.25 --steps 10 --warmup 2 --no-cpu-baseline
