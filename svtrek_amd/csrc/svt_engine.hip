@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.10.6 (gfx950, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.11.0 (gfx950, span walk + fused band, lane vote)"
 
 namespace {
 
@@ -151,7 +151,8 @@ __device__ __forceinline__ int lane_id() {
 #endif
     return l;
 }
-__device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
+// The lane mask of p straight from its compare (no v_cndmask / v_cmp round trip through a VGPR).
+__device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ __forceinline__ int32_t rdlane_i(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
@@ -1240,6 +1241,24 @@ struct StopList {
     uint32_t kw;
 };
 
+// One span event's test for window [s, e] (query beg = s-1): c = it is a candidate with value
+// val; brk = a leading-S read whose walk passes e (refine_end's stop search, :210-221).
+template <int KIND>
+__device__ __forceinline__ bool span_cand(const uint4 &v, uint32_t s, uint32_t e, int32_t beg32, uint32_t &val,
+                                          bool &brk) {
+    const uint32_t x = v.x, op = v.y & 0xfu, len = v.y >> 4;
+    const bool ovl = (int32_t)v.z > beg32;   // hts_itr_next overlap; pos < end holds below hi
+    brk = false;
+    val = x;
+    if (KIND == K_INS) return ovl && op == OP_INS && x <= e;                   // refinement.c:299
+    if (KIND == K_START) return ovl && x <= e && (op == OP_DEL || (op == SP_TRAIL && s <= x));   // :124 / :147-159
+    const bool lead = op == SP_LEAD && ovl && s <= x && x <= e;                // :210-220
+    const uint32_t wend = x + len;
+    brk = lead && wend > e;
+    val = op == OP_DEL ? x + len + 1u : wend + 1u;
+    return (ovl && x <= e && op == OP_DEL) || (lead && !brk);                  // :190-200
+}
+
 template <int KIND>
 __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t s, uint32_t e, int64_t lo, int64_t hi,
                                           uint64_t E0, uint64_t E1, uint64_t nslow, Sink &sink,
@@ -1265,21 +1284,10 @@ __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t 
         for (int u = 0; u < SPAN_U; u++) {
             if ((uint64_t)(u * WAVE) >= left) break;
             if ((uint64_t)(u * WAVE + ln) >= left) v[u] = make_uint4(0, 0, 0, 0);   // zero event: no candidate
-            const uint32_t x = v[u].x, op = v[u].y & 0xfu, len = v[u].y >> 4;
-            const bool ovl = (int32_t)v[u].z > beg32;   // hts_itr_next overlap; pos < end holds below hi
-            bool c, brk = false;
-            uint32_t val = x;
-            if (KIND == K_INS) {
-                c = ovl && op == OP_INS && x <= e;                                      // refinement.c:299
-            } else if (KIND == K_START) {
-                c = ovl && x <= e && (op == OP_DEL || (op == SP_TRAIL && s <= x));      // :124 / :147-159
-            } else {
-                const bool lead = op == SP_LEAD && ovl && s <= x && x <= e;            // :210-220
-                const uint32_t wend = x + len;
-                brk = lead && wend > e;
-                c = (ovl && x <= e && op == OP_DEL) || (lead && !brk);                  // :190-200
-                val = op == OP_DEL ? x + len + 1u : wend + 1u;
-            }
+            const uint32_t x = v[u].x;
+            bool brk;
+            uint32_t val;
+            const bool c = span_cand<KIND>(v[u], s, e, beg32, val, brk);
             const uint64_t m = ballot(c);
             const int32_t idx = cnt + (int32_t)mbcnt(m);
             if (c && idx < sink.cap) sink.buf[idx] = (int32_t)val;
@@ -2065,22 +2073,97 @@ constexpr uint32_t LV_NONE = 1u << 14;   // no window (INV / other types): NA
 
 template <int W>
 struct LaneLds {
-    union {
-        struct {
-            uint16_t stage[W * LV_S];      // parked queries (phase 0 -> 1), staged band offsets (1 -> 2)
-            struct {
-                struct {
-                    int32_t cand[CAP];      // phase 1 gather
-                    int32_t ncand;
-                } g;
-            } u;
-            LvMeta meta[W];
-            StopReq stops[LV_STOPS];
-            int32_t nstops;
-        } a;
-        WinLds full;                        // scratch the span gather is handed (it uses none)
-    };
+    uint16_t stage[W * LV_S];   // parked queries (phase 0 -> 1), band offsets (1 -> 2)
+    LvMeta meta[W];
+    StopReq stops[LV_STOPS];
+    int32_t nstops;
 };
+
+// Phase 1 of one window, wave-wide (A4-A7 + the band): the window's span events [E0, E0+len)
+// are tested 256 at a time (four 16-B loads per lane in flight; lane offsets relative to the
+// span, clamped, masked), and each candidate goes straight to the exact band of consensus_pos
+// (band_filter's rule, see there): members in (lo, hi) are written to the window's row as
+// 16-bit offsets from lo, and the four whole-multiset facts are OR-ed ballots.  Values are
+// walk positions < 2^29 + 1 (reads reaching 2^28 bases or position 2^29 are slow and carry
+// no events), so every candidate is >= 0 and within +-2^30: no int64 path is ever needed.
+// refine_end's breaking leading-S reads are queued for phase 1b (stop_lane).
+struct LaneBand {
+    int32_t n;        // candidates collected (before the stop searches)
+    int32_t nb;       // band members (> LV_CAP: the row overflowed)
+    uint32_t flags;   // LV_U0 | LV_LT | LV_LE0 | LV_GE0
+};
+
+// span_cand as lane masks, one compare per ballot (each folds into one v_cmp writing an SGPR
+// pair; the conditions are combined on the scalar unit).  refine_end's value is x + len + 1
+// for both of its candidate kinds (D: the position after the op + 1; leading S that does not
+// break: walk end + 1).
+template <int KIND>
+__device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, uint32_t e, int32_t beg32,
+                                                   uint64_t &brk) {
+    const uint32_t x = v.x, op = v.y & 0xfu;
+    const uint64_t ovl = ballot((int32_t)v.z > beg32), le = ballot(x <= e);
+    brk = 0;
+    if (KIND == K_INS) return ovl & le & ballot(op == OP_INS);                                  // refinement.c:299
+    if (KIND == K_START) return ovl & le & (ballot(op == OP_DEL) | (ballot(op == SP_TRAIL) & ballot(s <= x)));
+    const uint64_t lead = ovl & le & ballot(op == SP_LEAD) & ballot(s <= x);                    // :210-220
+    brk = lead & ballot(x + (v.y >> 4) > e);
+    return (ovl & le & ballot(op == OP_DEL)) | (lead & ~brk);                                   // :190-200
+}
+
+template <int KIND>
+__device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
+                                              int32_t pos, int32_t lo, int32_t hi, uint16_t *row, uint64_t cbase,
+                                              const StopList &defer) {
+    const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);
+    const int ln = lane_id();
+    const uint4 *ev = (KIND == K_INS ? P.spI : P.spD) + E0;   // wave-uniform base: 32-bit lane offsets
+    int32_t vmin = 0x7fffffff, vmax = -1;   // this lane's smallest / largest candidate (the facts, at the end)
+    int32_t n = 0, nb = 0;
+    for (uint32_t b = 0; b < len; b += SPAN_U * WAVE) {
+        const uint32_t left = len - b;
+        uint4 v[SPAN_U];
+#pragma unroll
+        for (int u = 0; u < SPAN_U; u++)   // unconditional (clamped): all four in flight at once
+            v[u] = ev[min(b + (uint32_t)(u * WAVE + ln), len - 1u)];
+#pragma unroll
+        for (int u = 0; u < SPAN_U; u++) {
+            if ((uint32_t)(u * WAVE) >= left) break;
+            const uint32_t rem = left - (uint32_t)(u * WAVE);
+            const uint64_t in = rem >= (uint32_t)WAVE ? ~0ull : (1ull << rem) - 1ull;   // lanes inside the span
+            uint64_t brk;
+            const uint64_t cm = span_cand_mask<KIND>(v[u], s, e, beg32, brk) & in;
+            const int32_t iv = (int32_t)(KIND == K_END ? v[u].x + (v[u].y >> 4) + 1u : v[u].x);
+            n += (int32_t)__popcll(cm);
+            const bool c = __builtin_amdgcn_inverse_ballot_w64(cm);
+            vmin = min(vmin, c ? iv : 0x7fffffff);
+            vmax = max(vmax, c ? iv : -1);
+            const uint64_t mb = cm & ballot(iv > lo) & ballot(iv < hi);
+            if (mb) {
+                const int32_t nm = (int32_t)__popcll(mb);
+                if (nb + nm <= LV_CAP && __builtin_amdgcn_inverse_ballot_w64(mb))
+                    row[nb + (int32_t)mbcnt(mb)] = (uint16_t)(iv - lo);
+                nb += nm;
+            }
+            if (KIND == K_END && SVT_DIAG != 3) {
+                brk &= in;
+                if (brk) {   // queued: searched for the whole chunk of windows at once (phase 1b)
+                    int32_t base = 0;
+                    if (ln == 0) base = atomicAdd(defer.cnt, (int32_t)__popcll(brk));
+                    base = rdlane_i(base, 0);
+                    const int32_t qi = base + (int32_t)mbcnt(brk);
+                    if (__builtin_amdgcn_inverse_ballot_w64(brk) && qi < defer.cap) {
+                        const uint64_t op0 = cbase + (uint64_t)(v[u].w - (uint32_t)cbase);
+                        defer.q[qi] = StopReq{(uint32_t)(op0 / ALIGN_OPS), v[u].x, e, defer.kw};
+                    }
+                }
+            }
+        }
+    }
+    // the whole multiset's facts (band_filter's u, n_lt, n_le, n_ge) from the lanes' extremes
+    const uint64_t mu = ballot(vmin <= pos + SV_MIN_LENGTH / 2), mlt = ballot(vmin < pos - SV_MIN_LENGTH / 2);
+    const uint64_t mle = ballot(vmin <= lo), mge = ballot(vmax >= hi);
+    return LaneBand{n, nb, (mu ? 0u : LV_U0) | (mlt ? LV_LT : 0u) | (mle ? 0u : LV_LE0) | (mge ? 0u : LV_GE0)};
+}
 
 template <int N>
 __device__ __forceinline__ void lane_sort(uint32_t (&x)[LV_CAP]) {   // ascending bitonic network, static indices
@@ -2294,19 +2377,24 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     if ((uint32_t)ln < cnt) {
         LvQuery q{};
         lane_query(a, g0 + (uint32_t)ln, q);
-        *reinterpret_cast<LvQuery *>(L.a.stage + (uint32_t)ln * LV_S) = q;
+        *reinterpret_cast<LvQuery *>(L.stage + (uint32_t)ln * LV_S) = q;
     }
-    if (ln == 0) L.a.nstops = 0;
+    if (ln == 0) L.nstops = 0;
     wave_sync();
-    if (SVT_DIAG == 6) return;   // diagnostic build: phase 0 only
+    if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
+        if ((uint32_t)ln < cnt) {
+            const LvQuery q = *reinterpret_cast<const LvQuery *>(L.stage + (uint32_t)ln * LV_S);
+            write_result(a, q.liw >> 1, q.liw & 1u, (uint32_t)q.kind ^ q.e0[0] ^ q.e1[0] ^ q.cb[0]);
+        }
+        return;
+    }
     // ---- phase 1: span walk + band filter per window (wave-wide)
     for (uint32_t kw = 0; kw < cnt; kw++) {
-        const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.a.stage + kw * LV_S);
+        const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.stage + kw * LV_S);
         const int32_t qk = uniform_i(qp->kind);
         const uint32_t li = (uint32_t)uniform_i((int32_t)qp->liw) >> 1, w = (uint32_t)uniform_i((int32_t)qp->liw) & 1u;
         const uint32_t s = (uint32_t)uniform_i((int32_t)qp->s), e = (uint32_t)uniform_i((int32_t)qp->e);
         const uint32_t imp = (uint32_t)uniform_i((int32_t)qp->imp);
-        const int32_t chrom = uniform_i(qp->chrom);
         const uint64_t E0 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[0]) |
                             (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[1]) << 32;
         const uint64_t E1 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e1[0]) |
@@ -2322,46 +2410,39 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         } else if (qk & LQ_REDO) {
             flags = LV_REDO;
         } else {
-            Sink sink{L.a.u.g.cand, CAP, &L.a.u.g.ncand};
-            const StopList defer{L.a.stops, &L.a.nstops, LV_STOPS, kw};
-            const int32_t ns0 = uniform_i(L.a.nstops);
-            if (ln == 0) L.a.u.g.ncand = 0;
-            wave_sync();
-            if (E1 > E0) {
-                if (kind == K_INS) span_walk<K_INS>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink);
-                else if (kind == K_START) span_walk<K_START>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink);
-                else span_walk<K_END>(a.pile, chrom - 1, s, e, 0, 0, E0, E1, 0, sink, cb, &defer);
-            }
-            wave_sync();
-            n = uniform_i(L.a.u.g.ncand);
-            const int32_t ns1 = uniform_i(L.a.nstops);
-            if (n > CAP || !SVT_LANE_VOTE || !band_ok || ns1 > LV_STOPS || SVT_DIAG == 7) {
-                flags = LV_REDO;
+            const StopList defer{L.stops, &L.nstops, LV_STOPS, kw};
+            const int32_t ns0 = uniform_i(L.nstops);
+            const int32_t pos = (int32_t)imp, bw = k.range + max(k.ci, 0);
+            constexpr int32_t LIM = 1 << 30;
+            const uint32_t len = (uint32_t)min(E1 - E0, (uint64_t)0x80000000u);
+            if (!band_ok || pos <= -LIM || pos >= LIM || len >= 0x80000000u || !SVT_LANE_VOTE || SVT_DIAG == 7) {
+                flags = LV_REDO;   // the band is off (or the lane vote is): the wave-wide path
             } else {
-                Band bd;
-                const int32_t nb = band_filter(L.a.u.g.cand, n, (int32_t)imp, k, bd);
-                if (!bd.on || !bd.f32 || nb > LV_CAP) {
-                    flags = LV_REDO;
-                } else {
-                    lo = bd.lo;
-                    if (ln < nb) L.a.stage[kw * LV_S + (uint32_t)ln] = (uint16_t)(L.a.u.g.cand[ln] - lo);
-                    flags = (uint32_t)nb | LV_PENDING | (bd.u == 0 ? LV_U0 : 0u) | (bd.n_lt > 0 ? LV_LT : 0u) |
-                            (bd.n_le == 0 ? LV_LE0 : 0u) | (bd.n_ge == 0 ? LV_GE0 : 0u);
+                lo = pos - bw;
+                LaneBand r{0, 0, LV_U0 | LV_LE0 | LV_GE0};
+                uint16_t *row = L.stage + kw * LV_S;
+                if (len) {
+                    if (kind == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, pos, lo, pos + bw, row, cb, defer);
+                    else if (kind == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, pos, lo, pos + bw, row, cb, defer);
+                    else r = lane_walk<K_END>(a.pile, s, e, E0, len, pos, lo, pos + bw, row, cb, defer);
                 }
+                n = r.n;
+                const int32_t ns1 = uniform_i(L.nstops);
+                flags = r.nb > LV_CAP || ns1 > LV_STOPS ? LV_REDO : (uint32_t)r.nb | LV_PENDING | r.flags;
+                n += ns1 - ns0;   // the deferred stop candidates count toward min_count
             }
-            n += ns1 - ns0;   // the deferred stop candidates count toward min_count
         }
-        if (ln == 0) L.a.meta[kw] = LvMeta{lo, (int32_t)imp, li << 1 | w, flags, n};
+        if (ln == 0) L.meta[kw] = LvMeta{lo, (int32_t)imp, li << 1 | w, flags, n};
         wave_sync();
     }
     // ---- phase 1b: the chunk's deferred stop searches, one lane each, folded into their
     // windows' bands (counts by LDS atomics; band members appended to the staging rows)
     {
-        const int32_t nsq = min(uniform_i(L.a.nstops), LV_STOPS);
+        const int32_t nsq = min(uniform_i(L.nstops), LV_STOPS);
         if (ln < nsq) {
-            const StopReq rq = L.a.stops[ln];
+            const StopReq rq = L.stops[ln];
             const int32_t v = (int32_t)stop_lane(a.pile, rq);
-            LvMeta &m = L.a.meta[rq.kw];
+            LvMeta &m = L.meta[rq.kw];
             const uint32_t fl = m.flags;
             if (fl & LV_PENDING) {
                 constexpr int32_t LIM = 1 << 30;
@@ -2376,19 +2457,28 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 if (set) atomicOr(&m.flags, set);
                 if (lo < v && v < hi) {
                     const uint32_t idx = atomicAdd(&m.flags, 1u) & 0xffu;   // nb is the low byte
-                    if (idx < (uint32_t)LV_CAP) L.a.stage[rq.kw * LV_S + idx] = (uint16_t)(v - lo);
+                    if (idx < (uint32_t)LV_CAP) L.stage[rq.kw * LV_S + idx] = (uint16_t)(v - lo);
                     else atomicOr(&m.flags, LV_REDO);
                 }
             }
         }
         wave_sync();
     }
-    if (SVT_DIAG == 8) return;   // diagnostic build: phases 0-1 only
+    if (SVT_DIAG == 8) {   // diagnostic build: phases 0-1 only (a checksum of their LDS output written out)
+        if ((uint32_t)ln < cnt) {
+            const LvMeta mt = L.meta[ln];
+            const uint32_t *row32 = reinterpret_cast<const uint32_t *>(L.stage + (uint32_t)ln * LV_S);
+            uint32_t h = mt.flags ^ (uint32_t)mt.n ^ (uint32_t)mt.lo;
+            for (int j = 0; j < LV_S / 2; j++) h = h * 31u + row32[j];
+            write_result(a, mt.liw >> 1, mt.liw & 1u, h);
+        }
+        return;
+    }
     // ---- phase 2: one lane per staged window
     uint64_t redo;   // phase 3's windows (the meta rows are overwritten by its gathers)
     {
         const bool mine = (uint32_t)ln < cnt;
-        const LvMeta mt = mine ? L.a.meta[ln] : LvMeta{0, 0, 0, 0, 0};
+        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0, 0};
         // decisions: no window or fewer than min_count candidates -> NA (refinement.c:43-45);
         // the wave-wide path; or this lane's vote
         const bool na = mine && ((mt.flags & LV_NONE) || (!(mt.flags & LV_REDO) && mt.n < k.min_count));
@@ -2400,7 +2490,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         if (any) {
             uint32_t x[LV_CAP];
             // lanes without a staged window use row 0 read-only (rows exist for LV_W lanes only)
-            uint16_t *row = L.a.stage + (pend ? (uint32_t)ln : 0u) * LV_S;
+            uint16_t *row = L.stage + (pend ? (uint32_t)ln : 0u) * LV_S;
             const uint32_t *row32 = reinterpret_cast<const uint32_t *>(row);
 #pragma unroll
             for (int j = 0; j < LV_CAP; j += 2) {   // two offsets per 4-byte LDS read
