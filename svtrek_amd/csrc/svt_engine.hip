@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.11.0 (gfx950, span walk + fused band, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.11.1 (gfx950, span walk + fused band, lane vote)"
 
 namespace {
 
@@ -2058,6 +2058,7 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
 // the chip with 32 per wave (svt_ctx::launch)
 constexpr int LV_CAP = 32;   // band elements a lane votes on
 constexpr int LV_S = 34;     // u16 per staged row (17 words: odd -> no bank conflicts)
+static_assert(LV_S > LV_CAP, "a staged row needs a spare slot past LV_CAP");
 constexpr int LV_WMAX = 1023;   // band half-width for 16-bit offsets and prefix sums (32 * 2046 < 2^16)
 constexpr uint32_t LV_PENDING = 1u << 8, LV_U0 = 1u << 9, LV_LT = 1u << 10, LV_LE0 = 1u << 11, LV_GE0 = 1u << 12,
                    LV_REDO = 1u << 13;
@@ -2129,23 +2130,23 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
         for (int u = 0; u < SPAN_U; u++) {
             if ((uint32_t)(u * WAVE) >= left) break;
             const uint32_t rem = left - (uint32_t)(u * WAVE);
-            const uint64_t in = rem >= (uint32_t)WAVE ? ~0ull : (1ull << rem) - 1ull;   // lanes inside the span
             uint64_t brk;
-            const uint64_t cm = span_cand_mask<KIND>(v[u], s, e, beg32, brk) & in;
+            uint64_t cm = span_cand_mask<KIND>(v[u], s, e, beg32, brk);
+            if (rem < (uint32_t)WAVE) {   // the span's last, partial slot: its lanes only
+                const uint64_t in = (1ull << rem) - 1ull;
+                cm &= in;
+                brk &= in;
+            }
             const int32_t iv = (int32_t)(KIND == K_END ? v[u].x + (v[u].y >> 4) + 1u : v[u].x);
             n += (int32_t)__popcll(cm);
             const bool c = __builtin_amdgcn_inverse_ballot_w64(cm);
             vmin = min(vmin, c ? iv : 0x7fffffff);
             vmax = max(vmax, c ? iv : -1);
             const uint64_t mb = cm & ballot(iv > lo) & ballot(iv < hi);
-            if (mb) {
-                const int32_t nm = (int32_t)__popcll(mb);
-                if (nb + nm <= LV_CAP && __builtin_amdgcn_inverse_ballot_w64(mb))
-                    row[nb + (int32_t)mbcnt(mb)] = (uint16_t)(iv - lo);
-                nb += nm;
-            }
+            // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone)
+            if (__builtin_amdgcn_inverse_ballot_w64(mb)) row[min(nb + (int32_t)mbcnt(mb), LV_CAP)] = (uint16_t)(iv - lo);
+            nb += (int32_t)__popcll(mb);
             if (KIND == K_END && SVT_DIAG != 3) {
-                brk &= in;
                 if (brk) {   // queued: searched for the whole chunk of windows at once (phase 1b)
                     int32_t base = 0;
                     if (ln == 0) base = atomicAdd(defer.cnt, (int32_t)__popcll(brk));
