@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.11.1 (gfx950, span walk + fused band, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.11.2 (gfx950, span walk + fused band, lane vote)"
 
 namespace {
 
@@ -2060,7 +2060,9 @@ constexpr int LV_CAP = 32;   // band elements a lane votes on
 constexpr int LV_S = 34;     // u16 per staged row (17 words: odd -> no bank conflicts)
 static_assert(LV_S > LV_CAP, "a staged row needs a spare slot past LV_CAP");
 constexpr int LV_WMAX = 1023;   // band half-width for 16-bit offsets and prefix sums (32 * 2046 < 2^16)
-constexpr uint32_t LV_PENDING = 1u << 8, LV_U0 = 1u << 9, LV_LT = 1u << 10, LV_LE0 = 1u << 11, LV_GE0 = 1u << 12,
+// LV_BELOW / LV_ABOVE: some candidate lies at or below the band's low end / at or above its high
+// end (with the band itself they give band_filter's whole-multiset facts, see lane_vote)
+constexpr uint32_t LV_PENDING = 1u << 8, LV_BELOW = 1u << 9, LV_ABOVE = 1u << 10,
                    LV_REDO = 1u << 13;
 
 struct LvMeta {
@@ -2084,14 +2086,15 @@ struct LaneLds {
 // are tested 256 at a time (four 16-B loads per lane in flight; lane offsets relative to the
 // span, clamped, masked), and each candidate goes straight to the exact band of consensus_pos
 // (band_filter's rule, see there): members in (lo, hi) are written to the window's row as
-// 16-bit offsets from lo, and the four whole-multiset facts are OR-ed ballots.  Values are
+// 16-bit offsets from lo, and whether any candidate lies at or below lo / at or above hi is
+// an OR-ed lane mask (with the band they give the whole-multiset facts, lane_vote).  Values are
 // walk positions < 2^29 + 1 (reads reaching 2^28 bases or position 2^29 are slow and carry
 // no events), so every candidate is >= 0 and within +-2^30: no int64 path is ever needed.
 // refine_end's breaking leading-S reads are queued for phase 1b (stop_lane).
 struct LaneBand {
     int32_t n;        // candidates collected (before the stop searches)
     int32_t nb;       // band members (> LV_CAP: the row overflowed)
-    uint32_t flags;   // LV_U0 | LV_LT | LV_LE0 | LV_GE0
+    uint32_t flags;   // LV_BELOW | LV_ABOVE
 };
 
 // span_cand as lane masks, one compare per ballot (each folds into one v_cmp writing an SGPR
@@ -2113,12 +2116,12 @@ __device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, u
 
 template <int KIND>
 __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
-                                              int32_t pos, int32_t lo, int32_t hi, uint16_t *row, uint64_t cbase,
+                                              int32_t lo, int32_t hi, uint16_t *row, uint64_t cbase,
                                               const StopList &defer) {
     const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);
     const int ln = lane_id();
     const uint4 *ev = (KIND == K_INS ? P.spI : P.spD) + E0;   // wave-uniform base: 32-bit lane offsets
-    int32_t vmin = 0x7fffffff, vmax = -1;   // this lane's smallest / largest candidate (the facts, at the end)
+    uint64_t below = 0, above = 0;   // candidates at or below lo / at or above hi
     int32_t n = 0, nb = 0;
     for (uint32_t b = 0; b < len; b += SPAN_U * WAVE) {
         const uint32_t left = len - b;
@@ -2139,10 +2142,10 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
             }
             const int32_t iv = (int32_t)(KIND == K_END ? v[u].x + (v[u].y >> 4) + 1u : v[u].x);
             n += (int32_t)__popcll(cm);
-            const bool c = __builtin_amdgcn_inverse_ballot_w64(cm);
-            vmin = min(vmin, c ? iv : 0x7fffffff);
-            vmax = max(vmax, c ? iv : -1);
-            const uint64_t mb = cm & ballot(iv > lo) & ballot(iv < hi);
+            const uint64_t gt = ballot(iv > lo), lt = ballot(iv < hi);
+            below |= cm & ~gt;
+            above |= cm & ~lt;
+            const uint64_t mb = cm & gt & lt;
             // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone)
             if (__builtin_amdgcn_inverse_ballot_w64(mb)) row[min(nb + (int32_t)mbcnt(mb), LV_CAP)] = (uint16_t)(iv - lo);
             nb += (int32_t)__popcll(mb);
@@ -2160,10 +2163,7 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
             }
         }
     }
-    // the whole multiset's facts (band_filter's u, n_lt, n_le, n_ge) from the lanes' extremes
-    const uint64_t mu = ballot(vmin <= pos + SV_MIN_LENGTH / 2), mlt = ballot(vmin < pos - SV_MIN_LENGTH / 2);
-    const uint64_t mle = ballot(vmin <= lo), mge = ballot(vmax >= hi);
-    return LaneBand{n, nb, (mu ? 0u : LV_U0) | (mlt ? LV_LT : 0u) | (mle ? 0u : LV_LE0) | (mge ? 0u : LV_GE0)};
+    return LaneBand{n, nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
 }
 
 template <int N>
@@ -2206,7 +2206,12 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int3
         const int32_t md = (l0 + h0) >> 1;
         if ((int32_t)B[md] > w + SV_MIN_LENGTH / 2) h0 = md; else l0 = md + 1;
     }
-    int32_t p = (fl & LV_U0) ? 0 : l0 == 0 ? -1 : l0 - 1;
+    // band_filter's whole-multiset facts: the band's own elements (B[0] its minimum) plus
+    // whether candidates lie below / above it
+    const bool below = fl & LV_BELOW, above = fl & LV_ABOVE;
+    const bool u0 = !below && l0 == 0;                                          // none <= pos+25
+    const bool lt = below || (nb > 0 && (int32_t)B[0] < w - SV_MIN_LENGTH / 2);   // some < pos-25
+    int32_t p = u0 ? 0 : l0 == 0 ? -1 : l0 - 1;
     if (nb == 0) p = -1;
     int32_t kk = p + 1, prev = 0;   // cluster [kk, i] below i, its offset sum S
     uint32_t S = 0;
@@ -2226,7 +2231,7 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int3
         }
     }
     // upper_bound(pos-25) (refinement.c:12-19): the full multiset's A[0] / A[n-1]
-    const int32_t q = (fl & LV_LT) ? ((fl & LV_LE0) ? 0 : nb) : ((fl & LV_GE0) ? nb - 1 : nb);
+    const int32_t q = lt ? (!below ? 0 : nb) : (!above ? nb - 1 : nb);
     int32_t m = q;   // cluster [i, m) above i
     S = 0;
     for (int32_t i = q; i < nb; i++) {                                       // :80
@@ -2420,12 +2425,12 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 flags = LV_REDO;   // the band is off (or the lane vote is): the wave-wide path
             } else {
                 lo = pos - bw;
-                LaneBand r{0, 0, LV_U0 | LV_LE0 | LV_GE0};
+                LaneBand r{0, 0, 0u};
                 uint16_t *row = L.stage + kw * LV_S;
                 if (len) {
-                    if (kind == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, pos, lo, pos + bw, row, cb, defer);
-                    else if (kind == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, pos, lo, pos + bw, row, cb, defer);
-                    else r = lane_walk<K_END>(a.pile, s, e, E0, len, pos, lo, pos + bw, row, cb, defer);
+                    if (kind == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, pos + bw, row, cb, defer);
+                    else if (kind == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, pos + bw, row, cb, defer);
+                    else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, pos + bw, row, cb, defer);
                 }
                 n = r.n;
                 const int32_t ns1 = uniform_i(L.nstops);
@@ -2447,14 +2452,11 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             const uint32_t fl = m.flags;
             if (fl & LV_PENDING) {
                 constexpr int32_t LIM = 1 << 30;
-                const int32_t pos = m.pos, lo = m.lo, hi = lo + 2 * (k.range + max(k.ci, 0));
-                uint32_t clr = 0, set = 0;
-                if (v <= pos + SV_MIN_LENGTH / 2) clr |= LV_U0;
-                if (v < pos - SV_MIN_LENGTH / 2) set |= LV_LT;
-                if (v <= lo) clr |= LV_LE0;
-                if (v >= hi) clr |= LV_GE0;
+                const int32_t lo = m.lo, hi = lo + 2 * (k.range + max(k.ci, 0));
+                uint32_t set = 0;
+                if (v <= lo) set |= LV_BELOW;
+                if (v >= hi) set |= LV_ABOVE;
                 if (v <= -LIM || v >= LIM || (lo < v && v < hi && v < 0)) set |= LV_REDO;
-                if (clr) atomicAnd(&m.flags, ~clr);
                 if (set) atomicOr(&m.flags, set);
                 if (lo < v && v < hi) {
                     const uint32_t idx = atomicAdd(&m.flags, 1u) & 0xffu;   // nb is the low byte
