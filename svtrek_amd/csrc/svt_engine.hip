@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.11.2 (gfx950, span walk + fused band, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.11.3 (gfx950, span walk + fused band, lane vote)"
 
 namespace {
 
@@ -2083,7 +2083,7 @@ struct LaneLds {
 };
 
 // Phase 1 of one window, wave-wide (A4-A7 + the band): the window's span events [E0, E0+len)
-// are tested 256 at a time (four 16-B loads per lane in flight; lane offsets relative to the
+// are tested 64 * LW_U at a time (LW_U 16-B loads per lane in flight; lane offsets relative to the
 // span, clamped, masked), and each candidate goes straight to the exact band of consensus_pos
 // (band_filter's rule, see there): members in (lo, hi) are written to the window's row as
 // 16-bit offsets from lo, and whether any candidate lies at or below lo / at or above hi is
@@ -2114,6 +2114,11 @@ __device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, u
     return (ovl & le & ballot(op == OP_DEL)) | (lead & ~brk);                                   // :190-200
 }
 
+#ifndef SVT_LW_U
+#define SVT_LW_U 4
+#endif
+constexpr int LW_U = SVT_LW_U;   // 64-event slots per step of lane_walk (loads in flight per lane)
+
 template <int KIND>
 __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
                                               int32_t lo, int32_t hi, uint16_t *row, uint64_t cbase,
@@ -2123,14 +2128,14 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
     const uint4 *ev = (KIND == K_INS ? P.spI : P.spD) + E0;   // wave-uniform base: 32-bit lane offsets
     uint64_t below = 0, above = 0;   // candidates at or below lo / at or above hi
     int32_t n = 0, nb = 0;
-    for (uint32_t b = 0; b < len; b += SPAN_U * WAVE) {
+    for (uint32_t b = 0; b < len; b += LW_U * WAVE) {
         const uint32_t left = len - b;
-        uint4 v[SPAN_U];
+        uint4 v[LW_U];
 #pragma unroll
-        for (int u = 0; u < SPAN_U; u++)   // unconditional (clamped): all four in flight at once
+        for (int u = 0; u < LW_U; u++)   // unconditional (clamped): all four in flight at once
             v[u] = ev[min(b + (uint32_t)(u * WAVE + ln), len - 1u)];
 #pragma unroll
-        for (int u = 0; u < SPAN_U; u++) {
+        for (int u = 0; u < LW_U; u++) {
             if ((uint32_t)(u * WAVE) >= left) break;
             const uint32_t rem = left - (uint32_t)(u * WAVE);
             uint64_t brk;
@@ -2223,8 +2228,8 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int3
         while (kk > 0 && (int32_t)B[kk - 1] >= a - ci) { kk--; S += B[kk]; }   // :61-64
         prev = a;
         const int32_t c = i - kk + 1;
-        const int32_t co = (int32_t)div_small(S + (uint32_t)(c / 2), (uint32_t)c);   // :65
         if (c > maxL) {                                                      // :67-76
+            const int32_t co = (int32_t)div_small(S + (uint32_t)(c / 2), (uint32_t)c);   // :65
             const int32_t d = ref_abs(w - co);
             if (d < ci) return lo + co;
             if (d < distL) { maxL = c; valL = lo + co; distL = d; }
@@ -2242,8 +2247,8 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int3
         while (m < nb && (int32_t)B[m] <= a + ci) { S += B[m]; m++; }        // :83-86
         prev = a;
         const int32_t c = m - i;
-        const int32_t co = (int32_t)div_small(S + (uint32_t)(c / 2), (uint32_t)c);
         if (c > maxR) {                                                      // :88-97
+            const int32_t co = (int32_t)div_small(S + (uint32_t)(c / 2), (uint32_t)c);   // :87
             const int32_t d = ref_abs(w - co);
             if (d < ci) return lo + co;
             if (d < distR) { maxR = c; valR = lo + co; distR = d; }
