@@ -2073,6 +2073,12 @@ struct LvMeta {
 };
 constexpr int LV_STOPS = 64;   // deferred stop searches per chunk
 constexpr uint32_t LV_NONE = 1u << 14;   // no window (INV / other types): NA
+// diagnostic build 11: why a window left the lane path (bits 16+), reported as its result
+#if SVT_DIAG == 11
+#define LV_WHY(r) ((uint32_t)(r) << 16)
+#else
+#define LV_WHY(r) 0u
+#endif
 
 template <int W>
 struct LaneLds {
@@ -2419,7 +2425,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         if (qk < 0) {
             flags = LV_NONE;
         } else if (qk & LQ_REDO) {
-            flags = LV_REDO;
+            flags = LV_REDO | LV_WHY(1);
         } else {
             const StopList defer{L.stops, &L.nstops, LV_STOPS, kw};
             const int32_t ns0 = uniform_i(L.nstops);
@@ -2427,7 +2433,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             constexpr int32_t LIM = 1 << 30;
             const uint32_t len = (uint32_t)min(E1 - E0, (uint64_t)0x80000000u);
             if (!band_ok || pos <= -LIM || pos >= LIM || len >= 0x80000000u || !SVT_LANE_VOTE || SVT_DIAG == 7) {
-                flags = LV_REDO;   // the band is off (or the lane vote is): the wave-wide path
+                flags = LV_REDO | LV_WHY(2);   // the band is off (or the lane vote is): the wave-wide path
             } else {
                 lo = pos - bw;
                 LaneBand r{0, 0, 0u};
@@ -2439,7 +2445,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 }
                 n = r.n;
                 const int32_t ns1 = uniform_i(L.nstops);
-                flags = r.nb > LV_CAP || ns1 > LV_STOPS ? LV_REDO : (uint32_t)r.nb | LV_PENDING | r.flags;
+                flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : ns1 > LV_STOPS ? LV_REDO | LV_WHY(4) : (uint32_t)r.nb | LV_PENDING | r.flags;
                 n += ns1 - ns0;   // the deferred stop candidates count toward min_count
             }
         }
@@ -2461,12 +2467,12 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 uint32_t set = 0;
                 if (v <= lo) set |= LV_BELOW;
                 if (v >= hi) set |= LV_ABOVE;
-                if (v <= -LIM || v >= LIM || (lo < v && v < hi && v < 0)) set |= LV_REDO;
+                if (v <= -LIM || v >= LIM || (lo < v && v < hi && v < 0)) set |= LV_REDO | LV_WHY(5);
                 if (set) atomicOr(&m.flags, set);
                 if (lo < v && v < hi) {
                     const uint32_t idx = atomicAdd(&m.flags, 1u) & 0xffu;   // nb is the low byte
                     if (idx < (uint32_t)LV_CAP) L.stage[rq.kw * LV_S + idx] = (uint16_t)(v - lo);
-                    else atomicOr(&m.flags, LV_REDO);
+                    else atomicOr(&m.flags, LV_REDO | LV_WHY(6));
                 }
             }
         }
@@ -2523,6 +2529,12 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         wave_sync();
     }
     // ---- the windows voted wave-wide go to refine_redo_kernel (rare: 0.6 % of cfg4's)
+    if (SVT_DIAG == 11) {   // diagnostic build: each left-over window's result = 0xF0000000 | its reason
+        const bool mine = (uint32_t)ln < cnt;
+        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0, 0};
+        if ((redo >> ln) & 1ull) write_result(a, mt.liw >> 1, mt.liw & 1u, 0xF0000000u | (mt.flags >> 16));
+        return;
+    }
     if (SVT_DIAG == 9) {   // diagnostic build: count them (status word bits 8+), nothing else
         if (ln == 0 && redo) atomicAdd(a.status, (int32_t)__popcll(redo) << 8);
         return;
