@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.11.3 (gfx950, span walk + fused band, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.11.4 (gfx950, span walk + fused band, lane vote)"
 
 namespace {
 
@@ -1240,6 +1240,13 @@ struct StopList {
     int32_t cap;
     uint32_t kw;
 };
+// The lane kernel's queue: the count is wave-uniform and only this wave appends, so it lives
+// in a scalar register (may exceed LV_STOPS: those windows take the wave-wide path).
+struct LaneStops {
+    StopReq *q;
+    int32_t n;
+    uint32_t kw;
+};
 
 // One span event's test for window [s, e] (query beg = s-1): c = it is a candidate with value
 // val; brk = a leading-S read whose walk passes e (refine_end's stop search, :210-221).
@@ -2066,7 +2073,7 @@ constexpr uint32_t LV_PENDING = 1u << 8, LV_BELOW = 1u << 9, LV_ABOVE = 1u << 10
                    LV_REDO = 1u << 13;
 
 struct LvMeta {
-    int32_t lo, pos;
+    int32_t lo;       // the band's low end (pos - w, w = range + max(ci, 0))
     uint32_t liw;     // li << 1 | w
     uint32_t flags;   // nb | LV_* bits
     int32_t n;        // candidates (min_count test)
@@ -2085,7 +2092,6 @@ struct LaneLds {
     uint16_t stage[W * LV_S];   // parked queries (phase 0 -> 1), band offsets (1 -> 2)
     LvMeta meta[W];
     StopReq stops[LV_STOPS];
-    int32_t nstops;
 };
 
 // Phase 1 of one window, wave-wide (A4-A7 + the band): the window's span events [E0, E0+len)
@@ -2128,7 +2134,7 @@ constexpr int LW_U = SVT_LW_U;   // 64-event slots per step of lane_walk (loads 
 template <int KIND>
 __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
                                               int32_t lo, int32_t hi, uint16_t *row, uint64_t cbase,
-                                              const StopList &defer) {
+                                              LaneStops &defer) {
     const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);
     const int ln = lane_id();
     const uint4 *ev = (KIND == K_INS ? P.spI : P.spD) + E0;   // wave-uniform base: 32-bit lane offsets
@@ -2162,11 +2168,9 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
             nb += (int32_t)__popcll(mb);
             if (KIND == K_END && SVT_DIAG != 3) {
                 if (brk) {   // queued: searched for the whole chunk of windows at once (phase 1b)
-                    int32_t base = 0;
-                    if (ln == 0) base = atomicAdd(defer.cnt, (int32_t)__popcll(brk));
-                    base = rdlane_i(base, 0);
-                    const int32_t qi = base + (int32_t)mbcnt(brk);
-                    if (__builtin_amdgcn_inverse_ballot_w64(brk) && qi < defer.cap) {
+                    const int32_t qi = defer.n + (int32_t)mbcnt(brk);
+                    defer.n += (int32_t)__popcll(brk);
+                    if (__builtin_amdgcn_inverse_ballot_w64(brk) && qi < LV_STOPS) {
                         const uint64_t op0 = cbase + (uint64_t)(v[u].w - (uint32_t)cbase);
                         defer.q[qi] = StopReq{(uint32_t)(op0 / ALIGN_OPS), v[u].x, e, defer.kw};
                     }
@@ -2326,28 +2330,32 @@ __device__ __forceinline__ uint32_t stop_lane(const DevPileup &P, const StopReq 
 constexpr int32_t LQ_REDO = 1 << 4;   // kind bit: the window takes the wave-wide path (slow reads / e >= 2^31)
 struct LvQuery {
     int32_t kind;          // K_* (| LQ_REDO), -1: no window (NA)
-    int32_t chrom;
-    uint32_t s, e, imp, liw;
-    uint32_t e0[2], e1[2], cb[2];   // span bounds [E0, E1), the contig's first arena offset
+    int32_t lo;            // the vote's band low end: pos - (range + max(ci, 0))
+    uint32_t s, e, liw, len;        // the window, li << 1 | w, its span's event count
+    uint32_t e0[2], cb[2];          // the span's first event, the contig's first arena offset
 };
 static_assert(sizeof(LvQuery) <= LV_S * 2, "LvQuery must fit a staging row");
 
-__device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, LvQuery &q) {
+__device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band_ok, LvQuery &q) {
     const DevPileup &P = a.pile;
     const KParams &k = a.prm;
     const uint32_t w = g >= a.n ? 1u : 0u, li = g - w * a.n;
     const svt_locus L = a.loci[li];
     q.kind = -1;
-    q.chrom = L.chrom;
     q.liw = li << 1 | w;
     const uint32_t pos = L.pos, end = L.end;
-    if (L.type == T_INS && w == 0) { q.kind = K_INS; q.s = pos - (uint32_t)k.median; q.e = pos + (uint32_t)k.median; q.imp = pos; }
-    else if (L.type == T_DEL && w == 0) { q.kind = K_START; q.s = pos - (uint32_t)k.wider; q.e = pos + (uint32_t)k.narrow; q.imp = pos; }
-    else if (L.type == T_DEL) { q.kind = K_END; q.s = end - (uint32_t)k.narrow; q.e = end + (uint32_t)k.narrow; q.imp = end; }
+    uint32_t imp = 0;
+    if (L.type == T_INS && w == 0) { q.kind = K_INS; q.s = pos - (uint32_t)k.median; q.e = pos + (uint32_t)k.median; imp = pos; }
+    else if (L.type == T_DEL && w == 0) { q.kind = K_START; q.s = pos - (uint32_t)k.wider; q.e = pos + (uint32_t)k.narrow; imp = pos; }
+    else if (L.type == T_DEL) { q.kind = K_END; q.s = end - (uint32_t)k.narrow; q.e = end + (uint32_t)k.narrow; imp = end; }
     // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250): NA, NA
     if (q.kind < 0) return;
-    if (q.e >= 0x80000000u) { q.kind |= LQ_REDO; return; }   // the exact per-read path (gather_span)
-    q.e0[0] = q.e0[1] = q.e1[0] = q.e1[1] = 0;   // empty span: no reads
+    // the exact per-read path (gather_span) for windows ending at or past 2^31; the wave-wide
+    // vote when the band is off (band_ok) or pos is beyond +-2^30 (int32 differences could wrap)
+    constexpr int32_t LIM = 1 << 30;
+    if (q.e >= 0x80000000u || !band_ok || (int32_t)imp <= -LIM || (int32_t)imp >= LIM) { q.kind |= LQ_REDO; return; }
+    q.lo = (int32_t)imp - (k.range + max(k.ci, 0));
+    q.len = 0;   // empty span: no reads
     const int tid = L.chrom - 1;
     const int64_t beg = (int64_t)(uint32_t)(q.s - 1u), qend = (int64_t)(uint32_t)(q.e - 1u);
     if (tid < 0 || tid >= P.n_targets || qend <= beg) return;   // A3: no reads
@@ -2370,10 +2378,11 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, LvQuery &
     if (lo >= hi) return;
     const uint64_t *off = q.kind == K_INS ? P.spoffI : P.spoffD;
     const uint64_t E0 = off[lo], E1 = off[hi];
-    if (P.slowpre[hi] != P.slowpre[lo]) { q.kind |= LQ_REDO; return; }   // slow reads: exact per-read replay
+    // slow reads: exact per-read replay; spans of 2^31 events or more: the wave-wide path
+    if (P.slowpre[hi] != P.slowpre[lo] || E1 - E0 >= 0x80000000ull) { q.kind |= LQ_REDO; return; }
     const uint64_t cb = q.kind == K_END ? P.off64[ra] : 0ull;
     q.e0[0] = (uint32_t)E0; q.e0[1] = (uint32_t)(E0 >> 32);
-    q.e1[0] = (uint32_t)E1; q.e1[1] = (uint32_t)(E1 >> 32);
+    q.len = (uint32_t)(E1 - E0);
     q.cb[0] = (uint32_t)cb; q.cb[1] = (uint32_t)(cb >> 32);
 }
 
@@ -2387,75 +2396,66 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     LaneLds<LV_W> &L = lds_all[wid];
     const KParams &k = a.prm;
     const uint32_t cnt = min((uint32_t)LV_W, nw - g0);
-    const bool band_ok = k.range > SV_MIN_LENGTH / 2 && k.range + max(k.ci, 0) <= LV_WMAX && k.ci >= -LV_WMAX;
+    const int32_t bw = k.range + max(k.ci, 0);   // the band's half-width
+    const bool band_ok = k.range > SV_MIN_LENGTH / 2 && bw <= LV_WMAX && k.ci >= -LV_WMAX && SVT_LANE_VOTE &&
+                         SVT_DIAG != 7;
     // ---- phase 0: every window's A2 + A3 at once, one lane each (the dependent loads of
     // locus -> bucket words -> pos/emax searches -> span bounds run once per LV_W windows),
     // parked in the window's staging row (read back before that row is written)
     if ((uint32_t)ln < cnt) {
         LvQuery q{};
-        lane_query(a, g0 + (uint32_t)ln, q);
+        lane_query(a, g0 + (uint32_t)ln, band_ok, q);
         *reinterpret_cast<LvQuery *>(L.stage + (uint32_t)ln * LV_S) = q;
     }
-    if (ln == 0) L.nstops = 0;
     wave_sync();
     if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
         if ((uint32_t)ln < cnt) {
             const LvQuery q = *reinterpret_cast<const LvQuery *>(L.stage + (uint32_t)ln * LV_S);
-            write_result(a, q.liw >> 1, q.liw & 1u, (uint32_t)q.kind ^ q.e0[0] ^ q.e1[0] ^ q.cb[0]);
+            write_result(a, q.liw >> 1, q.liw & 1u, (uint32_t)q.kind ^ q.e0[0] ^ q.len ^ q.cb[0]);
         }
         return;
     }
-    // ---- phase 1: span walk + band filter per window (wave-wide)
+    // ---- phase 1: span walk + band per window (wave-wide)
+    LaneStops stops{L.stops, 0, 0u};   // refine_end's deferred stop searches (phase 1b)
     for (uint32_t kw = 0; kw < cnt; kw++) {
         const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.stage + kw * LV_S);
         const int32_t qk = uniform_i(qp->kind);
-        const uint32_t li = (uint32_t)uniform_i((int32_t)qp->liw) >> 1, w = (uint32_t)uniform_i((int32_t)qp->liw) & 1u;
+        const uint32_t liw = (uint32_t)uniform_i((int32_t)qp->liw);
         const uint32_t s = (uint32_t)uniform_i((int32_t)qp->s), e = (uint32_t)uniform_i((int32_t)qp->e);
-        const uint32_t imp = (uint32_t)uniform_i((int32_t)qp->imp);
+        const int32_t lo = uniform_i(qp->lo);
+        const uint32_t len = (uint32_t)uniform_i((int32_t)qp->len);
         const uint64_t E0 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[0]) |
                             (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[1]) << 32;
-        const uint64_t E1 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e1[0]) |
-                            (uint64_t)(uint32_t)uniform_i((int32_t)qp->e1[1]) << 32;
         const uint64_t cb = (uint64_t)(uint32_t)uniform_i((int32_t)qp->cb[0]) |
                             (uint64_t)(uint32_t)uniform_i((int32_t)qp->cb[1]) << 32;
         wave_sync();   // the row may be overwritten from here on
-        const int kind = qk & 7;
         uint32_t flags = 0;
-        int32_t lo = 0, n = 0;
+        int32_t n = 0;
         if (qk < 0) {
             flags = LV_NONE;
         } else if (qk & LQ_REDO) {
-            flags = LV_REDO | LV_WHY(1);
+            flags = LV_REDO | LV_WHY(1);   // slow reads, a window past 2^31, the band off
         } else {
-            const StopList defer{L.stops, &L.nstops, LV_STOPS, kw};
-            const int32_t ns0 = uniform_i(L.nstops);
-            const int32_t pos = (int32_t)imp, bw = k.range + max(k.ci, 0);
-            constexpr int32_t LIM = 1 << 30;
-            const uint32_t len = (uint32_t)min(E1 - E0, (uint64_t)0x80000000u);
-            if (!band_ok || pos <= -LIM || pos >= LIM || len >= 0x80000000u || !SVT_LANE_VOTE || SVT_DIAG == 7) {
-                flags = LV_REDO | LV_WHY(2);   // the band is off (or the lane vote is): the wave-wide path
-            } else {
-                lo = pos - bw;
-                LaneBand r{0, 0, 0u};
-                uint16_t *row = L.stage + kw * LV_S;
-                if (len) {
-                    if (kind == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, pos + bw, row, cb, defer);
-                    else if (kind == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, pos + bw, row, cb, defer);
-                    else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, pos + bw, row, cb, defer);
-                }
-                n = r.n;
-                const int32_t ns1 = uniform_i(L.nstops);
-                flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : ns1 > LV_STOPS ? LV_REDO | LV_WHY(4) : (uint32_t)r.nb | LV_PENDING | r.flags;
-                n += ns1 - ns0;   // the deferred stop candidates count toward min_count
+            const int32_t ns0 = stops.n;
+            stops.kw = kw;
+            LaneBand r{0, 0, 0u};
+            uint16_t *row = L.stage + kw * LV_S;
+            if (len) {
+                if (qk == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, cb, stops);
+                else if (qk == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, cb, stops);
+                else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, cb, stops);
             }
+            flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : stops.n > LV_STOPS ? LV_REDO | LV_WHY(4)
+                                                                            : (uint32_t)r.nb | LV_PENDING | r.flags;
+            n = r.n + stops.n - ns0;   // the deferred stop candidates count toward min_count
         }
-        if (ln == 0) L.meta[kw] = LvMeta{lo, (int32_t)imp, li << 1 | w, flags, n};
+        if (ln == 0) L.meta[kw] = LvMeta{lo, liw, flags, n};
         wave_sync();
     }
     // ---- phase 1b: the chunk's deferred stop searches, one lane each, folded into their
     // windows' bands (counts by LDS atomics; band members appended to the staging rows)
     {
-        const int32_t nsq = min(uniform_i(L.nstops), LV_STOPS);
+        const int32_t nsq = min(stops.n, LV_STOPS);
         if (ln < nsq) {
             const StopReq rq = L.stops[ln];
             const int32_t v = (int32_t)stop_lane(a.pile, rq);
@@ -2463,7 +2463,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             const uint32_t fl = m.flags;
             if (fl & LV_PENDING) {
                 constexpr int32_t LIM = 1 << 30;
-                const int32_t lo = m.lo, hi = lo + 2 * (k.range + max(k.ci, 0));
+                const int32_t lo = m.lo, hi = lo + 2 * bw;
                 uint32_t set = 0;
                 if (v <= lo) set |= LV_BELOW;
                 if (v >= hi) set |= LV_ABOVE;
@@ -2492,7 +2492,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     uint64_t redo;   // phase 3's windows (the meta rows are overwritten by its gathers)
     {
         const bool mine = (uint32_t)ln < cnt;
-        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0, 0};
+        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0};
         // decisions: no window or fewer than min_count candidates -> NA (refinement.c:43-45);
         // the wave-wide path; or this lane's vote
         const bool na = mine && ((mt.flags & LV_NONE) || (!(mt.flags & LV_REDO) && mt.n < k.min_count));
@@ -2522,7 +2522,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             if (pend) {
 #pragma unroll
                 for (int j = 0; j < LV_CAP; j += 2) wrow[j >> 1] = x[j] | x[j + 1] << 16;
-                const int32_t r = lane_vote(row, nb, mt.pos - mt.lo, mt.lo, mt.flags, k);
+                const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k);
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
             }
         }
@@ -2531,7 +2531,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     // ---- the windows voted wave-wide go to refine_redo_kernel (rare: 0.6 % of cfg4's)
     if (SVT_DIAG == 11) {   // diagnostic build: each left-over window's result = 0xF0000000 | its reason
         const bool mine = (uint32_t)ln < cnt;
-        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0, 0};
+        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0};
         if ((redo >> ln) & 1ull) write_result(a, mt.liw >> 1, mt.liw & 1u, 0xF0000000u | (mt.flags >> 16));
         return;
     }
