@@ -38,7 +38,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.11.4 (gfx950, span walk + fused band, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.11.5 (gfx950, span walk + fused band, lane vote)"
 
 namespace {
 
@@ -2406,6 +2406,8 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         LvQuery q{};
         lane_query(a, g0 + (uint32_t)ln, band_ok, q);
         *reinterpret_cast<LvQuery *>(L.stage + (uint32_t)ln * LV_S) = q;
+        L.meta[ln].lo = q.lo;     // the window's meta row: what phase 0 knows,
+        L.meta[ln].liw = q.liw;   // phase 1 adds flags and n
     }
     wave_sync();
     if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
@@ -2420,7 +2422,6 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     for (uint32_t kw = 0; kw < cnt; kw++) {
         const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.stage + kw * LV_S);
         const int32_t qk = uniform_i(qp->kind);
-        const uint32_t liw = (uint32_t)uniform_i((int32_t)qp->liw);
         const uint32_t s = (uint32_t)uniform_i((int32_t)qp->s), e = (uint32_t)uniform_i((int32_t)qp->e);
         const int32_t lo = uniform_i(qp->lo);
         const uint32_t len = (uint32_t)uniform_i((int32_t)qp->len);
@@ -2449,7 +2450,10 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                                                                             : (uint32_t)r.nb | LV_PENDING | r.flags;
             n = r.n + stops.n - ns0;   // the deferred stop candidates count toward min_count
         }
-        if (ln == 0) L.meta[kw] = LvMeta{lo, liw, flags, n};
+        if (ln == 0) {
+            L.meta[kw].flags = flags;
+            L.meta[kw].n = n;
+        }
         wave_sync();
     }
     // ---- phase 1b: the chunk's deferred stop searches, one lane each, folded into their
