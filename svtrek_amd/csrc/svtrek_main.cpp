@@ -232,6 +232,17 @@ int audit(int argc, char **argv) {
     printf("[INFO] Started processing variation file.\n");
     fflush(stdout);
 
+    // The GPU contexts (HIP runtime start-up, code object load) open beside the ingest too
+    const int G = a.gpus;
+    std::vector<svt_ctx *> ctxs(G, nullptr);
+    std::vector<int> open_rc(G, 0);
+    std::thread ot([&] {
+        for (int g = 0; g < G; g++) open_rc[g] = svt_open(&a.prm, a.devices[g], &ctxs[g]);
+    });
+    auto close_all = [&] {
+        for (svt_ctx *c : ctxs)
+            if (c) svt_close(c);
+    };
     // BAM ingest and the VCF read + A1 parse are independent: the parse runs beside the ingest
     std::string vcf;
     bool vcf_ok = false;
@@ -246,8 +257,14 @@ int audit(int argc, char **argv) {
     svth_bam *bam = svth_bam_read(a.bam, a.threads, err, sizeof err);
     const double t_ingest = now_s();
     vt.join();
-    if (!bam) { fprintf(stderr, "[ERROR] %s\n", err); svth_vcf_free(pv); return 1; }
-    if (!vcf_ok) { fprintf(stderr, "[ERROR]: File couldn't be opened %s\n", a.vcf); svth_bam_free(bam); return 1; }
+    ot.join();
+    if (!bam) { fprintf(stderr, "[ERROR] %s\n", err); svth_vcf_free(pv); close_all(); return 1; }
+    if (!vcf_ok) {
+        fprintf(stderr, "[ERROR]: File couldn't be opened %s\n", a.vcf);
+        svth_bam_free(bam);
+        close_all();
+        return 1;
+    }
     svt_pileup_view view;
     svth_bam_view(bam, &view);
     size_t mlen = 0;
@@ -259,7 +276,6 @@ int audit(int argc, char **argv) {
 
     const double t_parse = now_s();
     std::vector<svt_result> res(loci.size());
-    const int G = a.gpus;
     std::vector<int> rc(G, 0);
     std::vector<std::string> gerr(G);
     std::vector<double> load_s(G, 0.0);
@@ -272,9 +288,9 @@ int audit(int argc, char **argv) {
         });
     }
     auto worker = [&](int g) {
-        svt_ctx *ctx = nullptr;
-        int s = svt_open(&a.prm, a.devices[g], &ctx);
-        if (s) { rc[g] = s; gerr[g] = "svt_open failed (HIP device?)"; return; }
+        svt_ctx *ctx = ctxs[g];
+        int s = open_rc[g];
+        if (s || !ctx) { rc[g] = s ? s : SVT_EDEVICE; gerr[g] = "svt_open failed (HIP device?)"; return; }
         const svt_locus *in = loci.data();
         svt_result *out = res.data();
         size_t n = loci.size();
@@ -297,6 +313,7 @@ int audit(int argc, char **argv) {
         }
         if (s) { rc[g] = s; gerr[g] = svt_last_error(ctx); }
         svt_close(ctx);
+        ctxs[g] = nullptr;
         if (!s && G > 1)
             for (size_t k = 0; k < sh.rows.size(); k++) res[sh.rows[k]] = sh.res[k];
     };
