@@ -8,19 +8,27 @@ contigs, 30x HiFi-like pileup) -- the configuration the >= 100k loci/s target is
 Every rank generates the same seeded workload; the loci are put in genomic order and rank g
 refines the g-th contiguous slice against only the reads its queries can reach
 (distributed.shard_workload), so the total work is fixed as N grows
-("scaling": "strong").  A step = one batched launch of the HIP engine over the rank's slice
-(svt_refine_device_records: pileup, loci and results resident in HBM) and, at N > 1, the one
-collective of the path: an RCCL gather to rank 0 of the slice's 16-B {vcf_index, start, end,
-pad} records, padded to ceil(N_total / N) rows; the gather of step i overlaps the launch of
-step i + 1 (double-buffered records).  Rank 0 prints ONE JSON line.
+("scaling": "strong").
 
-roofline (the timed kernel, refine_span_kernel): `achieved` = the span walk's algorithmic
-bytes per launch (svt_work.event_bytes, counted exactly by svt_count_work; DESIGN.md
-"Roofline") / the kernel's mean launch time from HIP events on the launch stream.  `ref_walk`
-keeps SURVEY.md §8(d)'s figure (the bytes the reference's CIGAR walk touches) against index
-build + launch time.  `traffic` = HBM bytes per launch from the committed rocprofv3 PMC passes
-of this engine version and workload (profiles/traffic.json, tools/make_traffic.py).
-cpu_baseline: the CPU oracle (restatement of the reference's tpool path) on rank 0's host cores.
+A step is the whole per-locus path from the resident columnar pileup to refined calls:
+  1. the device index build (svt_reindex: index_kernel<census>, range_scan_kernel,
+     index_kernel<emit> -- every read's CIGAR walked once, refinement.c:118-159/:184-221/:295-318),
+  2. one batched refine launch over the rank's slice (svt_refine_device_records:
+     refine_lane_kernel + refine_redo_kernel; loci and 16-B result records resident in HBM),
+  3. at N > 1, the one collective of the path: an RCCL gather to rank 0 of the slice's 16-B
+     {vcf_index, start, end, pad} records, padded to ceil(N_total / N) rows (the gather of step i
+     overlaps step i + 1; double-buffered records).
+Rank 0 prints ONE JSON line.
+
+roofline: `achieved` = SURVEY.md §8(d)'s algorithmic bytes of the step -- what the reference's
+per-window CIGAR walk touches, 24 B/locus + 12 B/yielded read + 4 B/CIGAR word walked, counted
+exactly by svt_count_work -- / the step's mean duration from HIP events on the launch stream.
+`phases` splits the step (index build, refine) with their own event timings, and
+`engine_bytes` prices the refine launch alone with the span walk's own bytes (svt_work
+.event_bytes).  `traffic` = HBM bytes per step from the committed rocprofv3 PMC passes of this
+engine version and workload, summed over the step's kernels (profiles/traffic.json,
+tools/make_traffic.py).  cpu_baseline: the CPU oracle (restatement of the reference's tpool
+path) on rank 0's host cores.
 """
 from __future__ import annotations
 
@@ -116,9 +124,13 @@ def _engine_version() -> str:
     return version()
 
 
+STEP_KERNELS = ("index_kernel<census>", "range_scan_kernel", "index_kernel<emit>", "refine_lane_kernel",
+                "refine_redo_kernel")
+
+
 def _traffic(workload: str, kernel: str, records: bool) -> tuple[int | None, str | None]:
-    """HBM bytes per launch of this engine version / workload / kernel from the committed
-    rocprofv3 PMC passes (tools/make_traffic.py -> profiles/traffic.json), or (None, None)."""
+    """HBM bytes per step of this engine version / workload from the committed rocprofv3 PMC
+    passes (tools/make_traffic.py -> profiles/traffic.json), or (None, None)."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
@@ -199,17 +211,18 @@ def main() -> int:
         eng.refine_device_records(d_loci.data_ptr(), n, pg.buffer(i).data_ptr(), d_index.data_ptr(), 0, sh)
 
     def step(i: int) -> None:
-        launch(i)
-        pg.submit(i)
+        eng.reindex(sh)   # the device index: every read's CIGAR walked once
+        launch(i)         # the batched refine over the rank's loci
 
     for i in range(args.warmup):
         step(i)
+        pg.submit(i)
     pg.drain()
     eng.sync(sh)
 
-    # HIP events on the launch stream: N = 1 -> one pair around the K launches (nothing else
-    # runs on that stream; / K = mean launch duration incl. the dispatch gap); N > 1 -> a pair
-    # per launch (gather waits are interleaved on the stream).
+    # HIP events on the launch stream: N = 1 -> one pair around the K steps (nothing else runs
+    # on that stream; / K = mean step duration incl. dispatch gaps); N > 1 -> a pair per step
+    # (gather waits are interleaved on the stream).
     per_launch = gather
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps if per_launch else 1)]
@@ -221,13 +234,11 @@ def main() -> int:
         ev[0][0].record(stream)
     for i in range(args.steps):
         if per_launch:
-            buf = pg.buffer(i)
             ev[i][0].record(stream)
-            eng.refine_device_records(d_loci.data_ptr(), n, buf.data_ptr(), d_index.data_ptr(), 0, sh)
+        step(i)
+        if per_launch:
             ev[i][1].record(stream)
-            pg.submit(i)
-        else:
-            step(i)
+        pg.submit(i)
     if not per_launch:
         ev[0][1].record(stream)
     pg.drain()
@@ -237,9 +248,9 @@ def main() -> int:
     wall = time.perf_counter() - t0
     eng.sync(sh)   # raises on a deferred spill-pool overflow
     if per_launch:
-        kern_mean_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        step_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     else:
-        kern_mean_ms = ev[0][0].elapsed_time(ev[0][1]) / args.steps
+        step_ms = ev[0][0].elapsed_time(ev[0][1]) / args.steps
 
     t_max = wall
     if world > 1:
@@ -255,43 +266,41 @@ def main() -> int:
         unpack_records(np.concatenate([p.cpu().numpy().view(np.uint32) for p in parts]), n_total)
         verified = True
 
-    # ---- untimed: per-launch durations, warm and with the Infinity Cache flushed first
-    pl = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
-    for a_, b_ in pl:
-        a_.record(stream)
-        launch(0)
-        b_.record(stream)
-    torch.cuda.synchronize(dev)
-    warm_ms = sorted(a_.elapsed_time(b_) for a_, b_ in pl)
+    # ---- untimed: the two phases on their own (5 runs each), and a step with the Infinity
+    # Cache flushed first
+    def timed_ms(fn, reps: int = 5) -> list[float]:
+        pl = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a_, b_ in pl:
+            a_.record(stream)
+            fn()
+            b_.record(stream)
+        torch.cuda.synchronize(dev)
+        return sorted(a_.elapsed_time(b_) for a_, b_ in pl)
+    index_ms = statistics.median(timed_ms(lambda: eng.reindex(sh)))
+    refine_ms = statistics.median(timed_ms(lambda: launch(0)))
     cold_ms = None
     if not args.no_cold:
         flush = torch.empty(1 << 30, dtype=torch.uint8, device=dev)   # 4x the 256 MiB MALL
         cold = []
         for k in range(3):
             flush.fill_(k + 1)
-            a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a_.record(stream)
-            launch(0)
-            b_.record(stream)
-            torch.cuda.synchronize(dev)
-            cold.append(a_.elapsed_time(b_))
+            cold += timed_ms(lambda: step(0), 1)
         cold_ms = statistics.median(cold)
         del flush
+    eng.sync(sh)
 
     total_loci = n_total * args.steps
     value = total_loci / t_max
+    ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]   # SURVEY 8(d)
+    achieved = ref_bytes / (step_ms * 1e-3) / 1e9
     ev_bytes = int(work["event_bytes"]) + 12 * n   # records: 16-B result record (not 8) + 4-B row index
-    achieved = ev_bytes / (kern_mean_ms * 1e-3) / 1e9
-    ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
-    ref_ms = kern_mean_ms + load_stats["index_ms"]
-    gather_variant = os.environ.get("SVTREK_GATHER", "span")
-    kernel = {"span": "refine_lane_kernel", "span1": "refine_span_kernel", "event": "refine_event_kernel",
-              "index": "refine_index_kernel"}.get(gather_variant, "refine_kernel")
-    if kernel == "refine_lane_kernel" and not os.environ.get("SVTREK_LANE_W") and 2 * n < 65536:
-        kernel = "refine_span_kernel"   # the engine's size-based pick (svt_engine.hip, launch)
-    traffic, traffic_src = _traffic(args.workload, kernel, records=True)
+    refine_kernel = "refine_lane_kernel" if (os.environ.get("SVTREK_GATHER", "span") != "span1" and
+                                             (os.environ.get("SVTREK_LANE_W") or 2 * n >= 65536)) \
+        else "refine_span_kernel"   # the engine's size-based pick (svt_engine.hip, launch)
+    traffic, traffic_src = _traffic(args.workload, "step", records=True)
     if args.scale != 1.0 or world > 1:
         traffic = traffic_src = None
+    idx_bytes = int(load_stats.get("index_bytes", 0))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -323,26 +332,36 @@ def main() -> int:
                        **({"loci_scale": args.scale} if args.scale != 1.0 else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_over_alg": round(traffic / ev_bytes, 4) if traffic else None,
-                         "traffic_gbs": round(traffic / (kern_mean_ms * 1e-3) / 1e9, 2) if traffic else None,
+                         "traffic_over_alg": round(traffic / ref_bytes, 4) if traffic else None,
+                         "traffic_gbs": round(traffic / (step_ms * 1e-3) / 1e9, 2) if traffic else None,
                          "traffic_source": traffic_src,
-                         "kernel": kernel, "kernel_ms_mean": round(kern_mean_ms, 5),
-                         "kernel_ms_timing": "per-launch event pairs" if per_launch else
-                         "one event pair around the timed launches / K",
-                         "kernel_ms_warm_min": round(warm_ms[0], 5),
-                         "kernel_ms_cold": round(cold_ms, 5) if cold_ms else None,
-                         "alg_bytes_per_launch": ev_bytes,
-                         "alg_bytes": ("span walk: 36 B/locus (16 in, 4 row index, 16 record out) + 32 B/query "
-                                       "+ 4 B/search entry + 16 B/span bounds + 16 B/span event + 36 B/stop search "
-                                       "+ 4 B/stop chunk word (svt_work)") if gather_variant == "span" else
-                                      f"{gather_variant} gather (svt_work.event_bytes)",
-                         "ref_walk": {"bytes": ref_bytes, "ms": round(ref_ms, 5),
-                                      "gbs": round(ref_bytes / (ref_ms * 1e-3) / 1e9, 2),
-                                      "note": "SURVEY 8(d) bytes of the reference's CIGAR walk / (device index "
-                                              "build + launch)"}},
-            "index_build": {"index_ms": load_stats["index_ms"], "load_ms": load_stats,
-                            "value_if_rebuilt_every_step": round(
-                                n_total / (t_max / args.steps + load_stats["index_ms"] * 1e-3), 1)},
+                         "kernel": "step = index build (" + ", ".join(STEP_KERNELS[:3]) + ") + refine (" +
+                                   (refine_kernel + (", refine_redo_kernel" if refine_kernel == "refine_lane_kernel"
+                                                     else "")) + ")",
+                         "step_ms_mean": round(step_ms, 5),
+                         "step_ms_timing": "per-step event pairs" if per_launch else
+                         "one event pair around the timed steps / K",
+                         "step_ms_cold": round(cold_ms, 5) if cold_ms else None,
+                         "alg_bytes_per_launch": ref_bytes,
+                         "alg_bytes": "SURVEY 8(d): 24 B/locus + 12 B/yielded read + 4 B/CIGAR word the reference "
+                                      "walk consumes (svt_count_work: windows, reads, ops_walked)",
+                         "phases": {
+                             "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
+                             "index_alg_bytes": idx_bytes,
+                             "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
+                             "index_bytes_def": "CIGAR stream twice (4 B/op), 36 B/read per pass, 32 B/read offsets, "
+                                                "16 B/span event, 144 B/lead block (svt_load_stats.index_bytes)",
+                         },
+                         "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
+                                          "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),
+                                          "kernel": refine_kernel,
+                                          "def": "the refine launch alone, priced with the span walk's own bytes: "
+                                                 "36 B/locus + 32 B/query + 4 B/search entry + 16 B/span bounds + "
+                                                 "16 B/span event + 36 B/stop search + 4 B/stop chunk word (svt_work)"}},
+            "index_build": {"index_ms_load": load_stats["index_ms"], "load_ms": load_stats,
+                            "value_index_resident": round(n_total / (refine_ms * 1e-3), 1),
+                            "note": "value_index_resident: loci/s of the refine launch alone, the index built once "
+                                    "(BAI-like amortisation); not the headline"},
             "cpu_baseline": cpu,
             "work": work,
             "records_verified": verified,

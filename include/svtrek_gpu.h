@@ -261,17 +261,30 @@ uint64_t   svt_poa_deferred(const svt_ctx *ctx);
 /* Bytes of device memory the loaded pileup occupies. */
 uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
 
-/* Where the last svt_load_pileup spent its time.  The device index (padded CIGAR arena,
- * chunk index, walk ends, candidate-op lists) depends only on the pileup, like the BAI
- * the reference's sam_itr_queryi needs (audit.c:271); it is built once per pileup and
- * reported here so that per-query throughput can be quoted with and without it. */
+/* Where the last svt_load_pileup spent its time.  The device index (per-read walk ends and
+ * slow flags, span-event offsets and lists, the lead arena of refine_end's stop searches)
+ * depends only on the pileup, like the BAI the reference's sam_itr_queryi needs
+ * (audit.c:271): it is the reference's per-read CIGAR walk (refinement.c:118-159 / :184-221 /
+ * :295-318) done once per read instead of once per (window, read). */
 typedef struct svt_load_stats {
-    double host_ms;      /* host pass: validation, prefix-max endpos, records, buckets          */
+    double host_ms;      /* host pass: validation, prefix-max endpos, records, buckets, ranges  */
     double upload_ms;    /* synchronous H2D copies of the caller's arrays (CIGAR words incl.)    */
-    double index_ms;     /* device index build: pack_kernel + event_kernel (HIP events)          */
+    double index_ms;     /* device index build: census + range scan + emit kernels (HIP events)  */
     double total_ms;     /* wall time of the whole svt_load_pileup call                          */
+    uint64_t index_bytes;   /* algorithmic bytes one index build moves: the CIGAR stream twice
+                               (4 B/op), per read 24 B read + 12 B written per pass and its 32 B of
+                               offsets, 16 B per span event, 144 B per 32-op lead arena block   */
+    uint64_t span_events;   /* D-list + I-list span events of the pileup                         */
+    uint64_t lead_blocks;   /* 32-op lead arena blocks (leading-S reads)                         */
+    uint64_t slow_reads;    /* reads whose walk reaches 2^28 bases or position 2^29              */
 } svt_load_stats;
 svt_status svt_last_load_stats(const svt_ctx *ctx, svt_load_stats *out);
+
+/* Rebuild the device index from the resident pileup on `hip_stream` (asynchronous, ordered
+ * after every launch of the context already issued): the same three kernels svt_load_pileup
+ * runs, no host work and no transfers.  Results of later refines are unchanged; bench.py
+ * times it as part of every step so that the step covers the whole per-read walk. */
+svt_status svt_reindex(svt_ctx *ctx, void *hip_stream);
 
 const char *svt_last_error(const svt_ctx *ctx);
 void        svt_close(svt_ctx *ctx);

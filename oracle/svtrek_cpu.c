@@ -189,6 +189,12 @@ svt_status svt_refine_device_records(svt_ctx *c, const svt_locus *d_loci, size_t
     return fail(c, SVT_EINVAL, "svt_refine_device_records: no device memory in the CPU backend");
 }
 svt_status svt_sync(svt_ctx *c, void *s) { (void)s; return c ? SVT_OK : SVT_EINVAL; }
+/* the CPU backend walks every read per query: it has no device index to rebuild */
+svt_status svt_reindex(svt_ctx *c, void *s) {
+    (void)s;
+    if (!c) return SVT_EINVAL;
+    return c->loaded ? SVT_OK : fail(c, SVT_ESTATE, "svt_reindex before svt_load_pileup");
+}
 void svt_poa_default_params(svt_poa_params *p) { if (p) memset(p, 0, sizeof *p); }
 uint64_t svt_pileup_ins_count(const svt_ctx *c) { (void)c; return 0; }
 svt_status svt_load_insseq(svt_ctx *c, const svt_insseq_view *s) {

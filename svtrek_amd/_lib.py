@@ -93,6 +93,10 @@ class SvtLoadStats(C.Structure):
         ("upload_ms", C.c_double),
         ("index_ms", C.c_double),
         ("total_ms", C.c_double),
+        ("index_bytes", C.c_uint64),
+        ("span_events", C.c_uint64),
+        ("lead_blocks", C.c_uint64),
+        ("slow_reads", C.c_uint64),
     ]
 
 
@@ -103,7 +107,7 @@ ENGINE_SYMBOLS = (
     "svt_sw_subwindows", "svt_sliding_window_ins",
     "svt_poa_default_params", "svt_pileup_ins_count", "svt_load_insseq", "svt_poa_consensus",
     "svt_poa_deferred", "svt_last_load_stats", "svt_open_multi", "svt_device_count",
-    "svt_refine_device_records",
+    "svt_refine_device_records", "svt_reindex",
 )
 
 _engine = None
@@ -148,6 +152,7 @@ def bind_abi(lib: C.CDLL) -> C.CDLL:
     lib.svt_refine_batch.argtypes = [P, P, C.c_size_t, P]
     lib.svt_refine_device.argtypes = [P, P, C.c_size_t, P, P]
     lib.svt_sync.argtypes = [P, P]
+    lib.svt_reindex.argtypes = [P, P]
     lib.svt_count_work.argtypes = [P, P, C.c_size_t, C.POINTER(SvtWork)]
     lib.svt_pileup_device_bytes.argtypes = [P]
     lib.svt_pileup_device_bytes.restype = C.c_uint64
@@ -169,7 +174,7 @@ def bind_abi(lib: C.CDLL) -> C.CDLL:
     lib.svt_poa_deferred.argtypes = [P]
     lib.svt_poa_deferred.restype = C.c_uint64
     for name in ("svt_open", "svt_open_multi", "svt_refine_device_records", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
-                 "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):
+                 "svt_reindex", "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):
         getattr(lib, name).restype = C.c_int32
     return lib
 

@@ -62,22 +62,35 @@ def load_shard(bam: str, loci: np.ndarray, prm, threads: int):
     return halo_slice(pl, loci, prm.wider_interval, prm.median_interval, prm.narrow_interval), info
 
 
-def run_rank(bam: str, loci: np.ndarray, prm, threads: int, refine, world: int, rank: int, device=None):
+def run_rank(bam: str, loci, prm, threads: int, refine, world: int, rank: int, device=None):
     """One rank's whole job: shard, region load, refine (refine(pileup, loci) -> results),
-    status agreement, gather.  Returns every result in VCF order on rank 0, None elsewhere."""
+    status agreement, gather.  Returns every result in VCF order on rank 0, None elsewhere.
+
+    `loci` may be the parsed array or a zero-argument callable that parses the VCF; every step
+    that can fail on one rank -- parsing, the engine (built lazily by `refine`), the BAM read,
+    the refinement, packing the gather records -- runs before the status all-reduce, so a
+    failing rank makes every rank raise instead of leaving the others blocked in a collective."""
     import torch
     import torch.distributed as dist
 
     from ._lib import RESULT_DTYPE
-    from .distributed import gather_results, shard_rows
-    rows = shard_rows(loci, world, rank)
-    mine = loci[rows]
+    from .distributed import pack_records, padded_rows, shard_rows, unpack_records
     err = None
+    rows = np.zeros(0, dtype=np.int64)
     local = np.zeros(0, dtype=RESULT_DTYPE)
+    payload = None
+    n_total = 0
     try:
+        if callable(loci):
+            loci = loci()
+        n_total = len(loci)
+        rows = shard_rows(loci, world, rank)
+        mine = loci[rows]
         if len(rows):
             pl, _ = load_shard(bam, mine, prm, threads)
             local = refine(pl, mine)
+        if world > 1:
+            payload = pack_records(rows, local, padded_rows(n_total, world))
     except Exception as e:   # noqa: BLE001 -- reported, then every rank stops together
         err = f"rank {rank}: {type(e).__name__}: {e}"
     if world > 1:
@@ -85,10 +98,17 @@ def run_rank(bam: str, loci: np.ndarray, prm, threads: int, refine, world: int, 
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
         if int(flag.item()):
             raise RuntimeError(err or f"rank {rank}: another rank failed")
-        return gather_results(rows, local, len(loci), device=device)
+        t = torch.from_numpy(payload.view(np.int32).copy())
+        if device is not None:
+            t = t.to(device)
+        parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+        dist.gather(t, parts, dst=0)
+        if rank != 0:
+            return None
+        return unpack_records(np.concatenate([p.cpu().numpy().view(np.uint32) for p in parts]), n_total)
     if err:
         raise RuntimeError(err)
-    out = np.empty(len(loci), dtype=RESULT_DTYPE)
+    out = np.empty(n_total, dtype=RESULT_DTYPE)
     out[rows] = local
     return out
 
@@ -121,23 +141,34 @@ def main(argv=None) -> int:
     if rank == 0:
         sys.stdout.write("[INFO] Started processing variation file.\n")
         sys.stdout.flush()
-    loci, msgs = parse_vcf(a.vcf, threads=max(1, a.t))
-    if rank == 0 and msgs:
-        sys.stderr.write(msgs)
     prm = Params(a.wider_interval, a.median_interval, a.narrow_interval, a.consensus_interval_range,
                  a.consensus_interval, a.consensus_min_count)
+    state = {}
+
+    def load_loci():   # parsed inside run_rank's guarded region (a bad VCF stops every rank)
+        loci, msgs = parse_vcf(a.vcf, threads=max(1, a.t))
+        state["loci"] = loci
+        if rank == 0 and msgs:
+            sys.stderr.write(msgs)
+        return loci
+
+    def refine(pl, mine):   # the engine is built on first use, inside the guarded region too
+        if "eng" not in state:
+            state["eng"] = Engine(prm, device=local)
+        state["eng"].load_pileup(pl)
+        return state["eng"].refine(mine)
+
     rc = 0
-    with Engine(prm, device=local) as eng:
-        def refine(pl, mine):
-            eng.load_pileup(pl)
-            return eng.refine(mine)
-        try:
-            res = run_rank(a.bam, loci, prm, max(1, a.t), refine, world, rank, device=dev)
-        except RuntimeError as e:
-            sys.stderr.write(f"[ERROR] {e}\n")
-            res, rc = None, 1
+    try:
+        res = run_rank(a.bam, load_loci, prm, max(1, a.t), refine, world, rank, device=dev)
+    except RuntimeError as e:
+        sys.stderr.write(f"[ERROR] {e}\n")
+        res, rc = None, 1
+    finally:
+        if "eng" in state:
+            state["eng"].close()
     if rank == 0 and rc == 0:
-        sys.stdout.write(host.format_batch(loci, res, threads=max(1, a.t)))
+        sys.stdout.write(host.format_batch(state["loci"], res, threads=max(1, a.t)))
         sys.stdout.write("[INFO] Ended processing variation file\n")
         sys.stdout.flush()
     if world > 1:

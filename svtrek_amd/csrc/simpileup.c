@@ -8,6 +8,7 @@
 #include "simpileup.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -251,6 +252,208 @@ static int cmp_key(const void *a, const void *b) {
     return (x->idx > y->idx) - (x->idx < y->idx);
 }
 
+
+/* Reads of contig t (its SVs sv[0..nsv), sorted by bp1) whose start lies before x_end,
+ * starting from x0, appended to b. 0 / -1 on OOM. */
+static int gen_contig(const sim_config *c, rng_t *rng, rbuf *b, const locus_t *sv, int32_t nsv, int32_t t, int32_t clen,
+                      double x0, double x_end) {
+    gen_t g = {c, rng, b, sv, nsv, t, clen};
+    int32_t cursor = 0;
+    double mean_gap = (double)c->read_len_mean / (c->coverage > 0 ? c->coverage : 1.0);
+    double x = x0;
+    for (;;) {
+        double u = rng_unif(rng);
+        if (u < 1e-300) u = 1e-300;
+        x += -log(u) * mean_gap;
+        if (x >= x_end) break;
+        int32_t qlen = (int32_t)(c->read_len_mean + c->read_len_sd * rng_norm(rng));
+        if (qlen < c->read_len_min) qlen = c->read_len_min;
+        int32_t start = (int32_t)x;
+        if (start < 0) { qlen += start; start = 0; if (qlen < 1) continue; }
+        while (cursor < g.nsv && g.sv[cursor].bp2 + 2 * c->bp_jitter + 2 < start) cursor++;
+        if (make_read(&g, start, qlen, &cursor)) return -1;
+    }
+    return 0;
+}
+
+static void rb_free(rbuf *b) { free(b->pos); free(b->flag); free(b->off); free(b->tid); free(b->ops); memset(b, 0, sizeof *b); }
+
+/* The reads of one contig -- reads [r0[q], r1[q]) of the buffers b[q], q < nb, in generation
+ * order -- sorted by pos (ties: generation order) into p's arrays from read w / op wo on. */
+static int emit_contig(sim_pileup *p, const rbuf *const *b, const int64_t *r0, const int64_t *r1, int nb, int64_t w,
+                       uint64_t wo) {
+    int64_t k = 0;
+    for (int q = 0; q < nb; q++) k += r1[q] - r0[q];
+    if (k > INT32_MAX) return -1;
+    sortkey_t *keys = (sortkey_t *)malloc((size_t)(k > 0 ? k : 1) * sizeof(sortkey_t));
+    int32_t *src = (int32_t *)malloc((size_t)(k > 0 ? k : 1) * sizeof(int32_t));   /* buffer of key i */
+    if (!keys || !src) { free(keys); free(src); return -1; }
+    int64_t i = 0;
+    for (int q = 0; q < nb; q++)
+        for (int64_t r = r0[q]; r < r1[q]; r++, i++) { keys[i].pos = b[q]->pos[r]; keys[i].idx = (int32_t)i; src[i] = q; }
+    qsort(keys, (size_t)k, sizeof(sortkey_t), cmp_key);
+    int64_t *base = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nb + 1));
+    if (!base) { free(keys); free(src); return -1; }
+    base[0] = 0;
+    for (int q = 0; q < nb; q++) base[q + 1] = base[q] + (r1[q] - r0[q]);
+    for (int64_t j = 0; j < k; j++) {
+        const int q = src[keys[j].idx];
+        const rbuf *bb = b[q];
+        const int64_t s = r0[q] + (keys[j].idx - base[q]);
+        uint64_t n = bb->off[s + 1] - bb->off[s];
+        memcpy(p->cigar + wo, bb->ops + bb->off[s], n * sizeof(uint32_t));
+        p->pos[w] = bb->pos[s];
+        p->flag[w] = bb->flag[s];
+        p->cig_off[w] = wo;
+        p->endpos[w] = endpos_of(bb->pos[s], bb->flag[s], p->cigar + wo, n);
+        wo += n;
+        w++;
+    }
+    free(keys); free(src); free(base);
+    return 0;
+}
+
+static int alloc_reads(sim_pileup *p, int64_t nr, uint64_t nops, int32_t nt) {
+    p->n_reads = nr;
+    p->n_ops = nops;
+    p->tid_off = (int64_t *)calloc((size_t)nt + 1, sizeof(int64_t));
+    p->pos = (int32_t *)malloc((size_t)(nr > 0 ? nr : 1) * sizeof(int32_t));
+    p->endpos = (int32_t *)malloc((size_t)(nr > 0 ? nr : 1) * sizeof(int32_t));
+    p->flag = (uint16_t *)malloc((size_t)(nr > 0 ? nr : 1) * sizeof(uint16_t));
+    p->cig_off = (uint64_t *)malloc((size_t)(nr + 1) * sizeof(uint64_t));
+    p->cigar = (uint32_t *)malloc((size_t)(nops > 0 ? nops : 1) * sizeof(uint32_t));
+    return p->tid_off && p->pos && p->endpos && p->flag && p->cig_off && p->cigar;
+}
+
+/* One PRNG stream for loci and then every contig in order (configs 1-4: the data of rounds 1-2). */
+static int gen_serial(const sim_config *c, sim_pileup *p, locus_t *L, int32_t per, rng_t *rng) {
+    rbuf b;
+    memset(&b, 0, sizeof b);
+    b.off = (uint64_t *)calloc(1, sizeof(uint64_t));
+    if (!b.off) return 0;
+    for (int32_t t = 0; t < c->n_targets; t++) {
+        int32_t n0 = t * per, n1 = (t + 1) * per;
+        if (n1 > c->n_loci) n1 = c->n_loci;
+        if (n0 > n1) n0 = n1;
+        qsort(L + n0, (size_t)(n1 - n0), sizeof(locus_t), cmp_locus);
+        /* starts drift in from before 0 */
+        if (gen_contig(c, rng, &b, L + n0, n1 - n0, t, p->contig_len[t], -(double)c->read_len_mean,
+                       (double)(p->contig_len[t] - 1))) { rb_free(&b); return 0; }
+    }
+    if (!alloc_reads(p, b.n, b.nops, c->n_targets)) { rb_free(&b); return 0; }
+    int64_t w = 0, r0 = 0;
+    uint64_t wo = 0;
+    for (int32_t t = 0; t < c->n_targets; t++) {   /* supplementaries were appended out of order */
+        int64_t r1 = r0;
+        while (r1 < b.n && b.tid[r1] == t) r1++;
+        p->tid_off[t] = w;
+        const rbuf *bp = &b;
+        if (emit_contig(p, &bp, &r0, &r1, 1, w, wo)) { rb_free(&b); return 0; }
+        wo += b.off[r1] - b.off[r0];
+        w += r1 - r0;
+        r0 = r1;
+    }
+    p->tid_off[c->n_targets] = w;
+    p->cig_off[w] = wo;
+    rb_free(&b);
+    return 1;
+}
+
+/* par_contigs = K > 0: every contig in K segments of read starts, each from its own PRNG
+ * stream (seeded from seed, contig and segment), one thread per segment -- configs too large
+ * to generate serially (cfg5: 9 G CIGAR ops).  A different pileup than K = 0, equally seeded. */
+typedef struct {
+    const sim_config *c;
+    sim_pileup *p;
+    const locus_t *sv;
+    int32_t nsv, t, k, K;
+    rbuf b;
+    int err;
+} seg_job;
+
+typedef struct {
+    sim_pileup *p;
+    seg_job *seg;   /* the contig's K segments */
+    int32_t K;
+    int64_t w;
+    uint64_t wo;
+    int err;
+} emit_job_t;
+
+static void *seg_run(void *arg) {
+    seg_job *j = (seg_job *)arg;
+    rng_t r;
+    rng_seed(&r, j->c->seed ^ (0x9e3779b97f4a7c15ull * (uint64_t)(j->t + 1)) ^ (0xbf58476d1ce4e5b9ull * (uint64_t)j->k));
+    const double clen = (double)(j->p->contig_len[j->t] - 1);
+    const double x0 = j->k == 0 ? -(double)j->c->read_len_mean : clen * j->k / j->K;
+    const double x1 = j->k + 1 == j->K ? clen : clen * (j->k + 1) / j->K;
+    j->b.off = (uint64_t *)calloc(1, sizeof(uint64_t));
+    j->err = !j->b.off || gen_contig(j->c, &r, &j->b, j->sv, j->nsv, j->t, j->p->contig_len[j->t], x0, x1);
+    return NULL;
+}
+
+static void *emit_run(void *arg) {
+    emit_job_t *j = (emit_job_t *)arg;
+    const rbuf *bs[64];
+    int64_t r0[64], r1[64];
+    for (int32_t q = 0; q < j->K; q++) { bs[q] = &j->seg[q].b; r0[q] = 0; r1[q] = j->seg[q].b.n; }
+    j->err = emit_contig(j->p, bs, r0, r1, j->K, j->w, j->wo) != 0;
+    for (int32_t q = 0; q < j->K; q++) rb_free(&j->seg[q].b);
+    return NULL;
+}
+
+static void run_all(void *(*fn)(void *), void *jobs, size_t size, int64_t n) {
+    pthread_t *th = (pthread_t *)calloc((size_t)(n > 0 ? n : 1), sizeof(pthread_t));
+    char *created = (char *)calloc((size_t)(n > 0 ? n : 1), 1);
+    for (int64_t i = 0; i < n; i++) {
+        void *a = (char *)jobs + (size_t)i * size;
+        if (th && created && pthread_create(&th[i], NULL, fn, a) == 0) created[i] = 1;
+        else fn(a);
+    }
+    for (int64_t i = 0; i < n; i++)
+        if (created && created[i]) pthread_join(th[i], NULL);
+    free(th);
+    free(created);
+}
+
+static int gen_parallel(const sim_config *c, sim_pileup *p, locus_t *L, int32_t per) {
+    const int32_t nt = c->n_targets, K = c->par_contigs > 64 ? 64 : c->par_contigs;
+    seg_job *S = (seg_job *)calloc((size_t)nt * (size_t)K, sizeof(seg_job));
+    emit_job_t *E = (emit_job_t *)calloc((size_t)nt, sizeof(emit_job_t));
+    if (!S || !E) { free(S); free(E); return 0; }
+    for (int32_t t = 0; t < nt; t++) {
+        int32_t n0 = t * per, n1 = (t + 1) * per;
+        if (n1 > c->n_loci) n1 = c->n_loci;
+        if (n0 > n1) n0 = n1;
+        qsort(L + n0, (size_t)(n1 - n0), sizeof(locus_t), cmp_locus);
+        for (int32_t k = 0; k < K; k++) S[t * K + k] = (seg_job){c, p, L + n0, n1 - n0, t, k, K, {0}, 0};
+    }
+    run_all(seg_run, S, sizeof(seg_job), (int64_t)nt * K);
+    int ok = 1;
+    int64_t nr = 0;
+    uint64_t nops = 0;
+    for (int32_t t = 0; t < nt; t++) {
+        E[t] = (emit_job_t){p, S + (size_t)t * K, K, nr, nops, 0};
+        for (int32_t k = 0; k < K; k++) {
+            ok &= !S[t * K + k].err;
+            nr += S[t * K + k].b.n;
+            nops += S[t * K + k].b.nops;
+        }
+    }
+    if (ok) ok = alloc_reads(p, nr, nops, nt);
+    if (ok) {
+        for (int32_t t = 0; t < nt; t++) p->tid_off[t] = E[t].w;
+        p->tid_off[nt] = nr;
+        p->cig_off[nr] = nops;
+        run_all(emit_run, E, sizeof(emit_job_t), nt);
+        for (int32_t t = 0; t < nt; t++) ok &= !E[t].err;
+    }
+    for (int64_t i = 0; i < (int64_t)nt * K; i++) rb_free(&S[i].b);
+    free(S);
+    free(E);
+    return ok;
+}
+
 sim_pileup *sim_generate(const sim_config *c) {
     if (!c || c->n_targets < 1 || c->n_loci < 0) return NULL;
     sim_pileup *p = (sim_pileup *)calloc(1, sizeof(sim_pileup));
@@ -288,75 +491,9 @@ sim_pileup *sim_generate(const sim_config *c) {
         p->truth[2 * k + 0] = bp1; p->truth[2 * k + 1] = bp2;
     }
 
-    rbuf b;
-    memset(&b, 0, sizeof b);
-    b.off = (uint64_t *)calloc(1, sizeof(uint64_t));
-    if (!b.off) { free(L); sim_free(p); return NULL; }
-    double mean_gap = (double)c->read_len_mean / (c->coverage > 0 ? c->coverage : 1.0);
-    for (int32_t t = 0; t < c->n_targets; t++) {
-        /* this contig's SVs, sorted by bp1 */
-        int32_t n0 = t * per, n1 = (t + 1) * per;
-        if (n1 > c->n_loci) n1 = c->n_loci;
-        if (n0 > n1) n0 = n1;
-        locus_t *sv = L + n0;
-        qsort(sv, (size_t)(n1 - n0), sizeof(locus_t), cmp_locus);
-        gen_t g = {c, &rng, &b, sv, n1 - n0, t, p->contig_len[t]};
-        int32_t cursor = 0;
-        double x = -(double)c->read_len_mean;   /* starts drift in from before 0 */
-        for (;;) {
-            double u = rng_unif(&rng);
-            if (u < 1e-300) u = 1e-300;
-            x += -log(u) * mean_gap;
-            if (x >= (double)(p->contig_len[t] - 1)) break;
-            int32_t qlen = (int32_t)(c->read_len_mean + c->read_len_sd * rng_norm(&rng));
-            if (qlen < c->read_len_min) qlen = c->read_len_min;
-            int32_t start = (int32_t)x;
-            if (start < 0) { qlen += start; start = 0; if (qlen < 1) continue; }
-            while (cursor < g.nsv && g.sv[cursor].bp2 + 2 * c->bp_jitter + 2 < start) cursor++;
-            if (make_read(&g, start, qlen, &cursor)) { free(L); free(b.pos); free(b.flag); free(b.off); free(b.tid); free(b.ops); sim_free(p); return NULL; }
-        }
-    }
+    int ok = c->par_contigs ? gen_parallel(c, p, L, per) : gen_serial(c, p, L, per, &rng);
     free(L);
-
-    /* sort reads per contig by pos (supplementaries were appended out of order) */
-    p->n_reads = b.n;
-    p->n_ops = b.nops;
-    sortkey_t *keys = (sortkey_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(sortkey_t));
-    p->tid_off = (int64_t *)calloc((size_t)c->n_targets + 1, sizeof(int64_t));
-    p->pos = (int32_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(int32_t));
-    p->endpos = (int32_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(int32_t));
-    p->flag = (uint16_t *)malloc((size_t)(b.n > 0 ? b.n : 1) * sizeof(uint16_t));
-    p->cig_off = (uint64_t *)malloc((size_t)(b.n + 1) * sizeof(uint64_t));
-    p->cigar = (uint32_t *)malloc((size_t)(b.nops > 0 ? b.nops : 1) * sizeof(uint32_t));
-    if (!keys || !p->tid_off || !p->pos || !p->endpos || !p->flag || !p->cig_off || !p->cigar) {
-        free(keys); free(b.pos); free(b.flag); free(b.off); free(b.tid); free(b.ops); sim_free(p); return NULL;
-    }
-    int64_t w = 0;
-    uint64_t wo = 0;
-    int64_t r0 = 0;
-    for (int32_t t = 0; t < c->n_targets; t++) {
-        int64_t r1 = r0;
-        while (r1 < b.n && b.tid[r1] == t) r1++;
-        int64_t k = 0;
-        for (int64_t i = r0; i < r1; i++, k++) { keys[k].pos = b.pos[i]; keys[k].idx = (int32_t)(i - r0); }
-        qsort(keys, (size_t)k, sizeof(sortkey_t), cmp_key);
-        p->tid_off[t] = w;
-        for (int64_t i = 0; i < k; i++) {
-            int64_t s = r0 + keys[i].idx;
-            uint64_t n = b.off[s + 1] - b.off[s];
-            memcpy(p->cigar + wo, b.ops + b.off[s], n * sizeof(uint32_t));
-            p->pos[w] = b.pos[s];
-            p->flag[w] = b.flag[s];
-            p->cig_off[w] = wo;
-            p->endpos[w] = endpos_of(b.pos[s], b.flag[s], p->cigar + wo, n);
-            wo += n;
-            w++;
-        }
-        r0 = r1;
-    }
-    p->tid_off[c->n_targets] = w;
-    p->cig_off[w] = wo;
-    free(keys); free(b.pos); free(b.flag); free(b.off); free(b.tid); free(b.ops);
+    if (!ok) { sim_free(p); return NULL; }
     return p;
 }
 

@@ -36,6 +36,8 @@ typedef struct sim_config {
     double   p_noise_sv;       /* per read: one unrelated D/I >= 50 bp                   */
     double   p_clip_ends;      /* per read end: short soft clip / hard clip              */
     double   p_exotic;         /* per error op: N, H, P or a code 9..15 op (quirk coverage) */
+    int32_t  par_contigs;      /* != 0: each contig's reads from its own PRNG stream, one thread
+                                  per contig (a different, equally seeded pileup; 0: one stream) */
 } sim_config;
 
 typedef struct sim_pileup sim_pileup;

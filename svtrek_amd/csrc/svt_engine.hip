@@ -33,12 +33,13 @@
 #include <algorithm>
 #include <chrono>
 #include <new>
+#include <atomic>
 #include <thread>
 #include <vector>
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.11.5 (gfx950, span walk + fused band, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.12.0 (gfx950, stream index build, span walk, lane vote)"
 
 namespace {
 
@@ -51,24 +52,20 @@ constexpr int32_t T_INS = 1, T_DEL = 2;
 constexpr int BKT_SHIFT = 12;               // read-start bucket = 4096 bp
 constexpr uint32_t NCIG_MASK = 0x1fffffffu; // rec.z: n_cigar | slow << 29 | clip << 30
 constexpr uint32_t SLOW_BIT = 1u << 29;
-constexpr uint32_t CIGAR_PAD = 1040;        // zero words after the arena (tile over-read)
-// Arena alignment: every read's CIGAR starts on a multiple of ALIGN_OPS words (zero-word
-// padding = 0M ops: advance nothing, never a candidate).  The chunk index holds one word
-// per CHUNK ops of the padded arena.
+constexpr uint32_t STREAM_PAD = 1024;       // zero words after the CIGAR stream (index_kernel's slot over-read)
+// Lead arena (refine_end's stop searches, refinement.c:210-221): the CIGAR of every read whose
+// first op is S (and that is not slow), copied to a 32-op-aligned block, with a chunk index of
+// one word per CHUNK ops: the walk position after the chunk's last op (refinement.c:141).
 constexpr int CHUNK = 8;                    // ops per chunk
-constexpr int CPL = 4;                      // chunks per lane in the index walk
-constexpr int ALIGN_OPS = CHUNK * CPL;      // 32 ops: a lane's chunks belong to one read
+constexpr int ALIGN_OPS = 32;               // lead arena block: 4 chunk words = one 16-B load
 constexpr uint32_t CH_POS = 0x1fffffffu;    // chunk word: walk position after the chunk's last op
-constexpr uint32_t CH_HEAD = 1u << 29;      //   the chunk is a read's first chunk
-constexpr uint32_t CH_DEL = 1u << 30;       //   the chunk holds a D op with len > 50  (refinement.c:124,:190)
-constexpr uint32_t CH_INS = 1u << 31;       //   the chunk holds an I op with len >= 50 (refinement.c:299)
-constexpr uint32_t CHUNK_PAD = 1040;        // zero words after the chunk index (speculative tile over-read)
-constexpr uint64_t INDEX_LIMIT = 1ull << 29; // walks reaching 2^29 are flagged slow (chunk word has 29 position bits)
+constexpr uint32_t LEAD_PAD = 64;           // zero words after the lead arena / its chunk index
+constexpr uint64_t INDEX_LIMIT = 1ull << 29; // walks reaching position 2^29 are flagged slow
 constexpr uint64_t WALK_LIMIT = 1ull << 28;  // ... and so are walks of 2^28 bases or more (a span event's 28-bit field)
-// Span events (svt_load_pileup, span_kernel): every read's breakpoint events, 16 B each,
+// Span events (svt_load_pileup, index_kernel<true>): every read's breakpoint events, 16 B each,
 // self-contained {x, w, endpos, aux} so that a window is one filter over a contiguous span:
-//   D list: D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:190),
-//           SP_LEAD {pos, walk << 4 | SP_LEAD, endpos, arena offset low 32} for cigar[0] == S (:210),
+//   D list: SP_LEAD {pos, walk << 4 | SP_LEAD, endpos, lead arena block} for cigar[0] == S (:210),
+//           D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:190),
 //           SP_TRAIL {walk end, SP_TRAIL, endpos, 0} for cigar[n-1] == S (:120,:147);
 //   I list: I >= 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:299).
 constexpr uint32_t SP_TRAIL = 0xEu, SP_LEAD = 0xFu;   // op codes no candidate event carries
@@ -76,16 +73,15 @@ constexpr uint32_t SP_TRAIL = 0xEu, SP_LEAD = 0xFu;   // op codes no candidate e
 struct DevPileup {
     const int32_t *pos;       // [n_reads]
     const int32_t *emax;      // [n_reads] prefix max of endpos within the contig
-    const uint4 *rec;         // [n_reads] {pos, endpos, n_cig | slow<<29 | clip<<30, cig_off low 32}
-    const uint64_t *off64;    // [n_reads+1] cig_off
+    const uint4 *rec;         // [n_reads] {pos, endpos, n_cig | slow<<29 | clip<<30, 0}
+    const uint64_t *off64;    // [n_reads+1] read r's CIGAR = cigar[off64[r] .. off64[r] + n_cig)
     const int64_t *tid_off;   // [n_targets+1]
     const int64_t *bkt_off;   // [n_targets+1] start of each contig's bucket table
     const uint2 *bkt;         // {first read with pos >= b << BKT_SHIFT, first read with emax >= b << BKT_SHIFT}
-    const uint32_t *cigar;    // padded by CIGAR_PAD zero words
-    const uint32_t *chunk;    // [arena words / CHUNK] chunk index (CH_POS | CH_HEAD | CH_DEL | CH_INS)
-    const uint4 *rec2;        // [n_reads] {walk end, candidate-op count, first candidate op (ev[evoff[r]])}
-    const uint64_t *evoff;    // [n_reads] offset of the read's candidate ops in ev
-    const uint2 *ev;          // candidate ops of every read in op order: {walk position before the op, CIGAR word}
+    const uint32_t *cigar;    // the CIGAR stream (caller's words; one 0M word for n_cigar == 0 reads)
+    const uint32_t *lcig;     // lead arena (32-op blocks)
+    const uint32_t *lchunk;   // its chunk index (CH_POS words, 4 per block)
+    const uint2 *rec2;        // [n_reads] {walk end, candidate ops (D > 50 + I >= 50)}
     const uint64_t *spoffD;   // [n_reads+1] span events: read r's D-list events are spD[spoffD[r] .. spoffD[r+1])
     const uint64_t *spoffI;   // [n_reads+1]              its I-list events spI[spoffI[r] .. spoffI[r+1])
     const uint4 *spD;
@@ -201,22 +197,6 @@ __device__ __forceinline__ int32_t wave_scan_max(int32_t v) {
     return v;
 }
 
-// Inclusive segmented wave64 scan of (head, value): a head restarts the running sum.
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ void seg_step(uint32_t &h, uint32_t &v) {
-    uint32_t hs = dpp<CTRL, ROWMASK>(h), vs = dpp<CTRL, ROWMASK>(v);
-    v = h ? v : v + vs;
-    h |= hs;
-}
-__device__ __forceinline__ void wave_seg_scan(uint32_t &h, uint32_t &v) {
-    seg_step<0x111, 0xf>(h, v);
-    seg_step<0x112, 0xf>(h, v);
-    seg_step<0x114, 0xf>(h, v);
-    seg_step<0x118, 0xf>(h, v);
-    seg_step<0x142, 0xa>(h, v);
-    seg_step<0x143, 0xc>(h, v);
-}
-
 __device__ __forceinline__ int64_t wave_scan_add64(int64_t x) {
     int l = lane_id();
 #pragma unroll
@@ -265,7 +245,7 @@ struct Sink {
 
 struct WinStats {
     unsigned long long reads = 0, ops = 0;
-    // event walk's own reads (G_EVENT COUNT builds): see svt_work
+    // span walk's own reads (svt_count_work): see svt_work
     unsigned long long queries = 0, probe = 0, range = 0, lreads = 0, lentries = 0, stops = 0, stopch = 0;
     unsigned long long squeries = 0, span = 0;   // span walk (G_SPAN COUNT builds)
 };
@@ -386,548 +366,20 @@ __device__ __forceinline__ void gather_perread(const DevPileup &P, int tid, uint
     }
 }
 
-// ------------------------------------------------------------------ window stream
-// HBM layout (svt_load_pileup): every read's CIGAR starts on a multiple of OPL words and
-// is padded with zero words (0M: advances nothing, never a candidate) to the next
-// multiple, so each lane's OPL ops of a tile belong to exactly one read.
-#ifndef SVT_OPL
-#define SVT_OPL 8
-#endif
-#ifndef SVT_JUMP
-#define SVT_JUMP 1               // skip the rest of a read that broke / yields nothing
-#endif
-#ifndef SVT_EARLY_PREFETCH
-#define SVT_EARLY_PREFETCH 0     // prefetch the contiguous next tile before working on this one
-#endif
-constexpr int OPL = SVT_OPL;                // CIGAR ops per lane per tile (4, 8 or 16)
-constexpr int TILE = OPL * WAVE;            // 512 ops (2 KiB) per stream step at OPL 8
-
-struct StreamLds {
-    int8_t slot[WAVE + 4];   // per tile lane slot: block-relative index of the read starting there, else -1
-    uint2 walk[WAVE];        // read k: {walk start (pos, or inter.end+1 when it yields nothing), real op end}
-    uint2 meta[WAVE];        // read k: {pos, clip bits}
-};
-
-template <int KIND, bool COUNT>
-__device__ __forceinline__ void gather_stream(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
-                                              WinStats &st, StreamLds &L) {
-    // Positions in the stream stay below 2^32 (no wrap) when inter.end < 2^31 and every
-    // streamed read walks less than 2^31 (the others are flagged slow at load time).
-    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
-    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
-    int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi)) return;
-    const int ln = lane_id();
-    const uint64_t S0 = P.off64[lo];
-    const uint32_t base32 = (uint32_t)S0;
-    const uint32_t *cg = P.cigar;
-    const uint32_t dead_rp = e + 1u;   // walk start of reads that yield nothing: every op is past the break
-    uint32_t live_ops = 0;             // COUNT builds
-
-    for (int64_t rb = lo; rb < hi; rb += WAVE) {
-        // ---- one block of up to 64 reads, lane k <-> read rb + k
-        const int64_t r = rb + ln;
-        const bool inb = r < hi;
-        const uint4 rc = inb ? P.rec[r] : make_uint4(0, 0, 0, 0);
-        const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
-        const bool slow = (rc.z & SLOW_BIT) != 0;
-        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
-        const int32_t st0 = (int32_t)(rc.w - base32);              // stream-relative first op (multiple of OPL)
-        const int32_t en_pad = st0 + (int32_t)((ncig + (ALIGN_OPS - 1)) & ~(uint32_t)(ALIGN_OPS - 1));
-        const bool live = ovl && !slow && ncig > 0;
-        const int nblk = (int)min<int64_t>(WAVE, hi - rb);
-        const int32_t blk_end = rdlane_i(en_pad, nblk - 1);
-        wave_sync();
-        L.walk[ln] = make_uint2(live ? rpos : dead_rp, (uint32_t)(st0 + (int32_t)ncig));
-        L.meta[ln] = make_uint2(rpos, clip);
-
-        // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
-        if (KIND != K_INS) {
-            const bool z = ovl && ncig == 0 && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
-            if (KIND == K_START) sink.push(z && (clip & SVT_CLIP_LAST_S), (int32_t)rpos);       // :152
-            else sink.push(z && (clip & SVT_CLIP_FIRST_S), (int32_t)(rpos + 1u));                // :210-220
-        }
-        if (COUNT) {
-            st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
-            if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
-        }
-
-        const uint64_t live_m = ballot(live);
-        int32_t J = live_m ? rdlane_i(st0, __builtin_ctzll(live_m)) : blk_end;
-        uint32_t carry_rp = 0;
-        int32_t carry_k = -1;
-        uint4 cw[OPL / 4];
-#pragma unroll
-        for (int q = 0; q < OPL / 4; q++) cw[q] = make_uint4(0, 0, 0, 0);
-        if (J < blk_end) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)J + OPL * ln);
-#pragma unroll
-            for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
-        }
-        while (J < blk_end) {
-            const int32_t A = J;                             // tiles start on a read start or a tile end
-            const int32_t U = min(A + TILE, blk_end);
-            const int32_t jb = A + OPL * ln;                 // this lane's first op
-            const bool lane_ok = jb < U;
-            // ---- which lanes start a read
-            L.slot[ln] = -1;
-            if (ln == 0) L.slot[WAVE] = -1;
-            wave_sync();
-            if (ncig > 0 && inb && st0 >= A && st0 <= A + TILE) L.slot[(st0 - A) / OPL] = (int8_t)ln;
-            wave_sync();
-            const int32_t hk = lane_ok ? (int32_t)L.slot[ln] : -1;
-            const int32_t kinc = wave_scan_max(hk);
-            const int32_t kl = max(carry_k, kinc);           // this lane's read
-            const uint2 wk = L.walk[kl < 0 ? 0 : kl];       // {walk start, real end}
-
-            // ---- per op: reference advance and its running sum inside the lane
-            uint32_t wv[OPL];
-#pragma unroll
-            for (int q = 0; q < OPL / 4; q++) {
-                wv[4 * q] = cw[q].x; wv[4 * q + 1] = cw[q].y; wv[4 * q + 2] = cw[q].z; wv[4 * q + 3] = cw[q].w;
-            }
-#if SVT_EARLY_PREFETCH
-            // speculative prefetch of the contiguous next tile, issued before any work on this
-            // one; re-issued below only when the read at U turns out to be finished
-            if (U < blk_end) {
-                const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)U + OPL * ln);
-#pragma unroll
-                for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
-            }
-#endif
-            uint32_t Pi[OPL], T = 0, candm = 0;
-#pragma unroll
-            for (int i = 0; i < OPL; i++) {
-                const uint32_t op = wv[i] & 0xfu, len = wv[i] >> 4;
-                // bit `op` of ~0x12 (bits I=1, S=4 clear), sign-extended: all ones iff op advances rp
-                const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)~0x12u, op, 1);   // refinement.c:141
-                T += len & keep;
-                Pi[i] = T;
-                candm |= (uint32_t)is_candidate_op<KIND>(op, len) << i;
-            }
-            if (!lane_ok) { T = 0; candm = 0; }
-            // ---- wave: segmented scan of lane sums -> walk position before each lane
-            const uint32_t H = hk >= 0;
-            uint32_t Hi = H, Vi = H ? wk.x + T : T;
-            wave_seg_scan(Hi, Vi);
-            const uint32_t Hx = dpp<0x138, 0xf>(Hi), Vx = dpp<0x138, 0xf>(Vi);   // wave_shr:1
-            const uint32_t pre = H ? wk.x : (Hx ? Vx : carry_rp + Vx);
-            const uint32_t H63 = rdlane(Hi, WAVE - 1), V63 = rdlane(Vi, WAVE - 1);
-            const uint32_t next_carry_rp = H63 ? V63 : carry_rp + V63;
-            const int32_t next_carry_k = max(carry_k, rdlane_i(kinc, WAVE - 1));
-
-            // ---- next tile: continue the read at U unless it already broke / yields nothing;
-            //      otherwise jump to the next read that yields.  Prefetch it now.
-            int32_t Jn = U;
-            if (SVT_JUMP) {
-                const int32_t kc = next_carry_k;
-                const bool cont = kc >= 0 && U < rdlane_i(en_pad, kc);
-                if (!(cont && next_carry_rp <= e)) {
-                    const uint64_t later = kc >= 0 ? (live_m & ~((2ull << kc) - 1ull)) : live_m;
-                    Jn = later ? max(U, rdlane_i(st0, __builtin_ctzll(later))) : blk_end;
-                }
-            }
-            if (Jn < blk_end && (!SVT_EARLY_PREFETCH || Jn != U)) {   // cw is dead once wv is unpacked
-                const uint4 *src = reinterpret_cast<const uint4 *>(cg + S0 + (int64_t)Jn + OPL * ln);
-#pragma unroll
-                for (int q = 0; q < OPL / 4; q++) cw[q] = src[q];
-            }
-
-            // ---- walk positions: ops [0, nb) end at or before inter.end, op nb is the break
-            //      (refinement.c:145) when nb < OPL; positions only grow inside a read.
-            const bool lane_live = lane_ok && pre <= e;      // not past this read's break
-            uint32_t nb = 0;
-#pragma unroll
-            for (int i = 0; i < OPL; i++) nb += (pre + Pi[i] <= e) ? 1u : 0u;
-            const int32_t nreal = min(max((int32_t)wk.y - jb, 0), OPL);   // real (unpadded) ops here
-            const uint32_t livem = lane_live ? ((2u << nb) - 1u) & ((1u << OPL) - 1u) : 0u;
-            const bool brk = lane_live && (int32_t)nb < nreal;             // this lane holds the break op
-            const int32_t lr = (int32_t)wk.y - 1 - jb;                     // read's last real op, if here
-            const bool has_last = lane_live && lr >= 0 && lr < OPL && (uint32_t)lr < nb;   // reached, no break
-            if (COUNT) live_ops += lane_live ? (uint32_t)min((int32_t)nb + 1, nreal) : 0u;
-            const uint32_t pushm = candm & livem;
-            const bool stop = KIND != K_INS && (brk || has_last);
-            if (pushm || stop) {
-                // rare: candidates (A4-A6) and the soft-clip candidate of the read's stop op
-                const int32_t si = brk ? (int32_t)nb : lr;                 // stop op index
-                uint32_t stop_after = 0;
-#pragma unroll
-                for (int i = 0; i < OPL; i++) {
-                    const uint32_t before = pre + (i ? Pi[i - 1] : 0u), after = pre + Pi[i];
-                    if ((pushm >> i) & 1u) {
-                        const uint32_t len = wv[i] >> 4;
-                        sink.push1(KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before);   // :198 / :136
-                    }
-                    if (i == si) stop_after = after;
-                }
-                if (KIND != K_INS && stop) {
-                    const uint2 mt = L.meta[kl];
-                    if (KIND == K_START) {   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
-                        if (!brk && (mt.y & SVT_CLIP_LAST_S) && s <= stop_after) sink.push1((int32_t)stop_after);
-                        if (COUNT && brk && (int32_t)nb != lr) live_ops++;        // cigar[n-1] test word
-                    } else {                 // leading S and s <= pos <= e: walked rp + 1  (:210-220)
-                        if ((mt.y & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)mt.x && (int64_t)mt.x <= (int64_t)e)
-                            sink.push1((int32_t)(stop_after + 1u));
-                    }
-                }
-            }
-            carry_rp = next_carry_rp;
-            carry_k = next_carry_k;
-            J = Jn;
-        }
-        // reads whose walk could wrap uint32: exact per-read replay
-        uint64_t sm = ballot(ovl && slow);
-        while (sm) {
-            const int l = __builtin_ctzll(sm);
-            sm &= sm - 1;
-            walk_read<KIND, COUNT>(cg, S0 + (uint64_t)(int64_t)rdlane_i(st0, l), rdlane(ncig, l), rdlane(rpos, l),
-                                   rdlane(clip, l), s, e, sink, st);
-        }
-    }
-    if (COUNT) st.ops += rdlane(wave_scan_add(live_ops), WAVE - 1);
-}
-
-// ------------------------------------------------------------------ index walk (default)
-// The chunk index (built once by svt_load_pileup) holds, for every CHUNK = 8 ops of the
-// padded arena, the reference walk position after the chunk's last op (refinement.c:141:
-// rp += len unless I/S) and two flags: the chunk holds a DEL candidate op (D, len > 50) /
-// an INS candidate op (I, len >= 50).  A window's walk then streams 4 B per 8 ops instead
-// of 32 B: positions are monotone inside a read, so the break of refinement.c:145 is the
-// first chunk whose end position exceeds inter.end (counted, not scanned), and only
-// chunks that hold a candidate op -- plus, for refine_end's leading-soft-clip candidate,
-// the chunk holding the break op -- are fetched op by op.  Those are queued in LDS as
-// {chunk, chunk start position} and resolved in batches (one 32-B load per lane).
-constexpr int EVCAP = 256;                  // queued chunks per wave before a flush
-constexpr uint32_t EV_STOP = 1u << 31;      // queued chunk holds the break op (refine_end soft clip)
-constexpr int ITILE = ALIGN_OPS * WAVE;     // 2048 ops (256 chunk words, 1 KiB) per index tile
-
-constexpr uint32_t RD_LIVE = 1u, RD_STOP = 2u, RD_CLIPL = 4u;   // IndexLds::rd[k].y flags (| clip << 30)
-
-struct IndexLds {
-    uint4 rd[WAVE];          // read k of the block: {pos, RD_* flags | clip << 30, stream-relative end of its
-                             //   real ops, stream-relative first op}
-    uint2 ev[EVCAP];         // queued chunks: {stream-relative chunk | EV_STOP, walk position before it}
-    int32_t nev;             // queued chunk count (LDS-atomic slot allocation)
-};
-
-__device__ __forceinline__ uint32_t cw_word(const uint4 &v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
-
+// ------------------------------------------------------------------ shared helpers
 __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141: every op but I (1) and S (4)
     return (w >> 4) & (uint32_t)__builtin_amdgcn_sbfe((int)~0x12u, w & 0xfu, 1);
 }
 
-// Resolve queued chunks: replay the reference walk over the chunk's 8 ops from its start
-// position; candidates are the ops before the break (refinement.c:124-145 / :190-206 /
-// :299-316), a STOP chunk also yields refine_end's soft-clip candidate rp + 1 (:210-220).
-#ifndef SVT_RN
-#define SVT_RN 0                 // 1: prefetch the next block's records
-#endif
-#ifndef SVT_QSCAN
-#define SVT_QSCAN 0              // 1: queue slots from a wave prefix scan instead of LDS atomics
-#endif
 #ifndef SVT_DIAG
-#define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 2 = no chunk
-                                 // resolve (index walk), 3 = no refine_end stop search (event walk), 4 = no sort/vote,
-                                 // 5 = sort + prefix sums, no vote
+#define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 3 = no refine_end
+                                 // stop search, 4 = no sort/vote, 5 = sort + prefix sums, no vote
 #endif
-// LEAN: the mid-tile overflow flush (rare), which must leave the walk's registers alone:
-// one 16-B half of the chunk in flight at a time.
-template <int KIND, bool LEAN>
-__device__ __forceinline__ void flush_chunks(const uint32_t *__restrict__ cg, IndexLds &L, int nev, uint32_t e,
-                                             Sink &sink) {
-    if (SVT_DIAG == 2) return;
-    wave_sync();
-    for (int b = 0; b < nev; b += WAVE) {
-        const int i = b + lane_id();
-        if (i < nev) {
-            const uint2 en = L.ev[i];
-            const uint4 *src = reinterpret_cast<const uint4 *>(cg + (uint64_t)(en.x & ~EV_STOP) * CHUNK);
-            uint32_t rp = en.y;
-            bool done = false;
-            uint4 c1 = make_uint4(0, 0, 0, 0);
-            if (!LEAN) c1 = src[1];
-#pragma unroll
-            for (int h = 0; h < 2 && !done; h++) {
-                const uint4 c = h == 0 ? src[0] : (LEAN ? src[1] : c1);
-                const uint32_t w[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t op = w[k] & 0xfu, len = w[k] >> 4;
-                    if (is_candidate_op<KIND>(op, len)) sink.push1(KIND == K_END ? (int32_t)(rp + len + 1u) : (int32_t)rp);
-                    rp += ref_adv(w[k]);
-                    if (rp > e) {
-                        if (KIND == K_END && (en.x & EV_STOP)) sink.push1((int32_t)(rp + 1u));
-                        done = true;
-                        break;
-                    }
-                }
-            }
-        }
-    }
-    wave_sync();
-    if (lane_id() == 0) L.nev = 0;
-    wave_sync();
-}
 
-template <int KIND, bool COUNT>
-__device__ __forceinline__ void gather_index(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
-                                             WinStats &st, IndexLds &L) {
-    // Chunk positions are < 2^30 for every read the index walk takes (the others are
-    // flagged slow at load time); windows ending at or past 2^31 take the exact per-read path.
-    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
-    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
-    int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi)) return;
-#if SVT_DIAG == 1
-    if (lo < hi) return;          // diagnostic build: region query only
-#endif
-    const int ln = lane_id();
-    // one dependent step: the stream base and the first block's records
-    const uint64_t S0 = P.off64[lo];                 // multiple of ALIGN_OPS
-    int64_t rb = lo;
-    uint4 rc = rb + ln < hi ? P.rec[rb + ln] : make_uint4(0, 0, 0, 0);
-#if SVT_RN
-    uint4 rn = rb + WAVE + ln < hi ? P.rec[rb + WAVE + ln] : make_uint4(0, 0, 0, 0);
-#endif
-    const uint32_t base32 = (uint32_t)S0;
-    const uint32_t *cg = P.cigar + S0;               // stream-relative CIGAR words
-    const uint32_t *cx = P.chunk + S0 / CHUNK;        // stream-relative chunk words
-    uint32_t live_ops = 0;                            // COUNT builds
-    int nev = 0;                                      // queued chunks (wave-uniform)
 
-    // ---- per-block state: lane k <-> read rb + k
-    int32_t st0 = 0, en_pad = 0, blk_end = 0, J = 0, Rb = -1;
-    uint64_t live_m = 0, slow_m = 0;
-    uint32_t carry_E = 0;
-    if (ln == 0) L.nev = 0;
-    auto open_block = [&]() {
-        const bool inb = rb + ln < hi;
-        const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
-        const bool slow = (rc.z & SLOW_BIT) != 0;
-        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;  // hts_itr_next overlap; pos < end below hi
-        st0 = (int32_t)(rc.w - base32);                        // stream-relative first op (multiple of 32)
-        en_pad = st0 + (int32_t)max((ncig + (ALIGN_OPS - 1)) & ~(uint32_t)(ALIGN_OPS - 1), (uint32_t)ALIGN_OPS);
-        const bool live = ovl && !slow && ncig > 0;
-        const int nblk = (int)min<int64_t>(WAVE, hi - rb);
-        blk_end = rdlane_i(en_pad, nblk - 1);
-        // refine_end's leading-soft-clip candidate needs the walk position after the break
-        // op (refinement.c:210-220): only reads with cigar[0] == S and s <= pos <= e
-        const bool stop = KIND == K_END && live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos &&
-                          (int64_t)rpos <= (int64_t)e;
-        const bool clipl = KIND == K_START && (clip & SVT_CLIP_LAST_S);
-        wave_sync();
-        L.rd[ln] = make_uint4(rpos, (live ? RD_LIVE : 0u) | (stop ? RD_STOP : 0u) | (clipl ? RD_CLIPL : 0u) | (clip << 30),
-                              (uint32_t)(st0 + (int32_t)ncig), (uint32_t)st0);
-        wave_sync();
-        // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
-        if (KIND != K_INS) {
-            const bool z = ovl && ncig == 0 && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
-            if (KIND == K_START) sink.push(z && (clip & SVT_CLIP_LAST_S), (int32_t)rpos);       // :152
-            else sink.push(z && (clip & SVT_CLIP_FIRST_S), (int32_t)(rpos + 1u));                // :210-220
-        }
-        if (COUNT) {
-            st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
-            if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
-        }
-        live_m = ballot(live);
-        slow_m = ballot(ovl && slow);
-        if (live_m) {
-            const int k0 = __builtin_ctzll(live_m);
-            J = rdlane_i(st0, k0);
-            Rb = k0 - 1;
-        } else {
-            J = blk_end;
-        }
-        carry_E = 0;
-    };
-    auto close_block = [&]() {
-        // reads whose walk could leave the chunk index's range: exact per-read replay
-        uint64_t sm = slow_m;
-        while (sm) {
-            const int l = __builtin_ctzll(sm);
-            sm &= sm - 1;
-            const uint4 q = L.rd[l];
-            walk_read<KIND, COUNT>(P.cigar, S0 + (uint64_t)q.w, uniform_i((int32_t)(q.z - q.w)), uniform_i((int32_t)q.x),
-                                   uniform_i((int32_t)(q.y >> 30)), s, e, sink, st);
-        }
-    };
-    // Move to the next block holding a read that yields; false when the window is done.
-    auto next_block = [&]() -> bool {
-        for (;;) {
-            close_block();
-            rb += WAVE;
-            if (rb >= hi) return false;
-#if SVT_RN
-            rc = rn;
-            rn = rb + WAVE + ln < hi ? P.rec[rb + WAVE + ln] : make_uint4(0, 0, 0, 0);
-#else
-            rc = rb + ln < hi ? P.rec[rb + ln] : make_uint4(0, 0, 0, 0);
-#endif
-            open_block();
-            if (J < blk_end) return true;
-        }
-    };
-    auto load_tile = [&](int32_t at) { return reinterpret_cast<const uint4 *>(cx + at / CHUNK)[ln]; };
-
-    // One tile [J, U = min(J + ITILE, blk_end)) from `cw`; sets J to the next tile's start
-    // (or blk_end when the block is finished).  Every read occupies whole 32-op lane groups
-    // whose first chunk carries CH_HEAD, so a lane's read is Rb + (heads at lanes <= it).
-    auto tile = [&](const uint4 cw) {
-        const int32_t A = J;
-        const int32_t U = min(A + ITILE, blk_end);
-        const int32_t jb = A + ALIGN_OPS * ln;           // this lane's first op
-        const int nok = (U - A) / ALIGN_OPS;             // lanes inside the tile (1..64)
-        const bool lane_ok = ln < nok;
-        const bool head = lane_ok && (cw.x & CH_HEAD);
-        const uint64_t hm = ballot(head);
-        const int32_t kl = Rb + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u)) +
-                           (head ? 1 : 0);
-        const uint2 wk = reinterpret_cast<const uint2 *>(&L.rd[lane_ok ? kl : 0])[0];   // {pos, RD_* flags}
-        const uint32_t E[CPL] = {cw.x & CH_POS, cw.y & CH_POS, cw.z & CH_POS, cw.w & CH_POS};
-        // walk position before this lane's first chunk: the read's pos at its head lane,
-        // else the previous lane's last chunk end (lane 0: the previous tile's)
-        const uint32_t prevE = dpp<0x138, 0xf>(E[CPL - 1]);   // wave_shr:1
-        const uint32_t start0 = head ? wk.x : (ln == 0 ? carry_E : prevE);
-
-        // ---- next tile: continue the read at U unless it already broke / yields nothing;
-        //      otherwise jump to the next read that yields (its first group is a head)
-        const int32_t kc = rdlane_i(kl, nok - 1);                 // read holding the last op before U
-        const uint32_t E_U = rdlane(E[CPL - 1], nok - 1);          // its walk position at U
-        const bool U_end = U == blk_end || U == rdlane_i(en_pad, kc);
-        int32_t Jn, Rn = kc;
-        if (!U_end && ((live_m >> kc) & 1ull) && E_U <= e) {
-            Jn = U;
-        } else {
-            const uint64_t later = live_m & ~((2ull << kc) - 1ull);
-            if (later) {
-                const int kn = __builtin_ctzll(later);
-                Jn = rdlane_i(st0, kn);
-                Rn = kn - 1;
-            } else {
-                Jn = blk_end;
-            }
-        }
-
-        // ---- this lane's chunks: [0, nb) end at or before inter.end; chunk nb (if any)
-        //      holds the break op (refinement.c:145); later chunks are dead.  Padding chunks
-        //      repeat the read's last position, so a chunk ending past inter.end is real.
-        const bool lane_live = lane_ok && (wk.y & RD_LIVE) && start0 <= e;
-        uint32_t nb = 0;
-#pragma unroll
-        for (int i = 0; i < CPL; i++) nb += E[i] <= e ? 1u : 0u;
-        const bool brk = lane_live && nb < (uint32_t)CPL;
-        // the read's last lane group: the next group starts a read (or U ends it)
-        const bool next_head = ln + 1 < nok ? ((hm >> (ln + 1)) & 1ull) != 0 : (ln + 1 == nok && U_end);
-        const bool has_last = lane_live && next_head && nb == (uint32_t)CPL;   // reached, no break
-        const uint32_t flag = KIND == K_INS ? CH_INS : CH_DEL;
-        const bool stop_q = KIND == K_END && brk && (wk.y & RD_STOP);
-        uint32_t qm = 0;
-        if (lane_live) {
-#pragma unroll
-            for (int i = 0; i < CPL; i++)
-                if ((uint32_t)i <= nb && (cw_word(cw, i) & flag)) qm |= 1u << i;
-            if (stop_q) qm |= 1u << nb;
-        }
-        if (has_last) {
-            const uint32_t rp_end = E[CPL - 1];           // walk position after the read's last op
-            if (KIND == K_START) {   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
-                if ((wk.y & RD_CLIPL) && s <= rp_end) sink.push1((int32_t)rp_end);
-            } else if (KIND == K_END) {   // leading S, s <= pos <= e: rp + 1 (refinement.c:210-220)
-                if (wk.y & RD_STOP) sink.push1((int32_t)(rp_end + 1u));
-            }
-        }
-        if (COUNT && lane_live) {
-            const int32_t wz = (int32_t)L.rd[kl].z;                         // real op end
-            const int32_t rem = wz - jb;                                   // real ops from this lane on
-            live_ops += (uint32_t)min((int32_t)nb * CHUNK, rem);
-            if (brk) {   // ops of the break chunk up to and including the break op
-                const uint32_t *w = cg + jb + (int32_t)nb * CHUNK;
-                uint32_t rp = nb ? E[nb - 1] : start0;
-                int k = 0;
-                while (k < CHUNK) { rp += ref_adv(w[k]); k++; if (rp > e) break; }
-                live_ops += (uint32_t)k;
-                if (KIND == K_START && jb + (int32_t)nb * CHUNK + k != wz) live_ops++;   // cigar[n-1] test
-            }
-        }
-        // ---- queue the chunks to resolve op by op (slots from an LDS atomic counter)
-        if (ballot(qm != 0)) {
-            int tot = 0;
-#pragma unroll
-            for (int i = 0; i < CPL; i++) tot += __popcll(ballot((qm >> i) & 1u));
-            if (nev + tot > EVCAP) { flush_chunks<KIND, true>(cg, L, nev, e, sink); nev = 0; }
-#if SVT_QSCAN
-            {
-                const uint32_t nq = (uint32_t)__popc(qm);
-                int o = nev + (int)(wave_scan_add(nq) - nq);
-#else
-            if (qm) {
-                int o = atomicAdd(&L.nev, __popc(qm));
-#endif
-                uint32_t m = qm;
-                while (m) {
-                    const int i = __builtin_ctz(m);
-                    m &= m - 1;
-                    const uint32_t cs = i ? E[i - 1] : start0;   // walk position before chunk i
-                    L.ev[o++] = make_uint2((uint32_t)(jb / CHUNK + i) | (stop_q && (uint32_t)i == nb ? EV_STOP : 0u), cs);
-                }
-            }
-            nev += tot;
-        }
-        carry_E = E_U;
-        Rb = Rn;
-        J = Jn;
-    };
-
-    // Two tile buffers in flight (ping-pong, static registers): while one tile is walked, the
-    // next one's chunk words (exact, or a guess that the stream continues contiguously, into
-    // the next block too) are already loading; a wrong guess costs one reload.
-    open_block();
-    if (J >= blk_end && !next_block()) { if (nev) flush_chunks<KIND, false>(cg, L, nev, e, sink); return; }
-    uint4 b0 = load_tile(J), b1;
-    int32_t t1;
-    {
-        const int32_t g = min(J + ITILE, blk_end);
-        b1 = load_tile(g);
-        t1 = g;
-    }
-    int32_t t0 = J;
-    // step: walk `cur` (holds tile J); make `nxt` hold the next tile, refill `cur` with a guess
-    auto step = [&](uint4 &cur, int32_t &tc, uint4 &nxt, int32_t &tn) -> bool {
-        tile(cur);
-        if (J >= blk_end && !next_block()) return false;
-        if (tn != J) { nxt = load_tile(J); tn = J; }
-        const int32_t g = min(J + ITILE, blk_end);
-        cur = load_tile(g);
-        tc = g;
-        return true;
-    };
-    (void)t0;
-    for (;;) {
-        if (!step(b0, t0, b1, t1)) break;
-        if (!step(b1, t1, b0, t0)) break;
-    }
-    if (nev) flush_chunks<KIND, false>(cg, L, nev, e, sink);
-    if (COUNT) st.ops += rdlane(wave_scan_add(live_ops), WAVE - 1);
-}
-
-// ------------------------------------------------------------------ event walk (default)
-// A read's walk (refinement.c:118-159 / :184-221 / :295-318) only matters to the vote
-// through (1) its candidate ops processed before the break and (2) the walk position at the
-// break or at the end, for the soft-clip candidates.  Both come from per-read summaries built
-// once by svt_load_pileup, independent of any query:
-//   * the read's candidate ops in op order, each with the walk position before it (`ev`):
-//     op i is processed iff that position is <= inter.end (positions only grow along the
-//     read, refinement.c:145), so a window takes the prefix of the list at or below inter.end;
-//   * the walk end (rec2.x): the read breaks iff walk end > inter.end;
-//   * the chunk index, searched (one 64-lane probe per 256 chunks) only when refine_end needs
-//     the position after the break op (leading soft clip, refinement.c:210-220) or when the
-//     work is counted.
-// So a window costs O(reads + candidate ops), independent of CIGAR length.
-
-// Walk position after the break op of a read that breaks (walk end > e): the first op whose
-// walk position after it exceeds e.  Wave-cooperative, uniform arguments; `op_idx` receives
-// the break op's index in the read.
+// Walk position after the break op of a leading-S read that breaks (walk end > e): the first
+// op whose walk position after it exceeds e, from the read's lead arena block at op0.
+// Wave-cooperative, uniform arguments; `op_idx` receives the break op's index in the read.
 __device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0, uint32_t ncig, uint32_t rpos,
                                                 uint32_t e, uint32_t &op_idx) {
     const int ln = lane_id();
@@ -936,7 +388,7 @@ __device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0
     uint32_t bc = nch, before = rpos;   // break chunk, walk position before it
     for (uint32_t b = 0; b < nch; b += 4 * WAVE) {
         const uint32_t c = b + 4u * (uint32_t)ln;
-        const uint4 q = c < nch ? *reinterpret_cast<const uint4 *>(P.chunk + c0 + c) : make_uint4(0, 0, 0, 0);
+        const uint4 q = c < nch ? *reinterpret_cast<const uint4 *>(P.lchunk + c0 + c) : make_uint4(0, 0, 0, 0);
         const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
         uint32_t first = 4;
 #pragma unroll
@@ -957,7 +409,7 @@ __device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0
         before = rdlane(E[3], WAVE - 1);   // chunk b + 4*64 - 1 ends here (all <= e)
     }
     // the break op inside chunk bc: lanes 0-7 take its ops
-    const uint32_t w = ln < CHUNK ? P.cigar[op0 + (uint64_t)bc * CHUNK + (uint32_t)ln] : 0u;
+    const uint32_t w = ln < CHUNK ? P.lcig[op0 + (uint64_t)bc * CHUNK + (uint32_t)ln] : 0u;
     const uint32_t after = before + wave_scan_add(ln < CHUNK ? ref_adv(w) : 0u);
     const uint64_t m = ballot(ln < CHUNK && after > e);
     const int k = __builtin_ctzll(m);   // exists: the chunk ends past e
@@ -968,10 +420,10 @@ __device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0
 // Row-parallel form of break_after for refine_end's soft-clip stops: up to 4 breaking reads
 // at once, one 16-lane row each (DPP row shifts never cross a row).  Lanes of row g take
 // read `l` = the g-th set bit of `m` (block lane), consume those bits, and push after + 1.
-// A read's arena offset is its contig's first offset `cbase` plus rec.w's 32-bit difference
-// (a contig's arena spans < 2^31 words, svt_load_pileup), so no off64 load is on this path.
-__device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t cbase, uint64_t m, uint32_t ncig_v,
-                                              uint32_t rpos_v, uint32_t offlo_v, uint32_t e, Sink &sink) {
+// The read's lead arena block comes with its SP_LEAD event (blk_v), so no per-read load is on
+// this path.
+__device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t m, uint32_t ncig_v, uint32_t rpos_v,
+                                              uint32_t blk_v, uint32_t e, Sink &sink) {
     const int ln = lane_id(), g = ln >> 4, t = ln & 15;
     int my = -1;
 #pragma unroll
@@ -985,8 +437,8 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t cbase
     // per-row read parameters (a bpermute from the read's block lane)
     const uint32_t ncig = (uint32_t)__shfl((int)ncig_v, has ? my : 0, WAVE);
     const uint32_t rpos = (uint32_t)__shfl((int)rpos_v, has ? my : 0, WAVE);
-    const uint32_t offlo = (uint32_t)__shfl((int)offlo_v, has ? my : 0, WAVE);
-    const uint64_t op0 = has ? cbase + (uint64_t)(offlo - (uint32_t)cbase) : 0ull;
+    const uint32_t blk = (uint32_t)__shfl((int)blk_v, has ? my : 0, WAVE);
+    const uint64_t op0 = has ? (uint64_t)blk * ALIGN_OPS : 0ull;
     const uint64_t c0 = op0 / CHUNK;
     const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
     bool found = false;
@@ -994,7 +446,7 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t cbase
     for (uint32_t it = 0;; it += 64) {   // 64 chunks (16 lanes x 4) per row per step
         const uint32_t c = it + 4u * (uint32_t)t;
         const bool act = has && !found && c < nch;
-        const uint4 q = act ? *reinterpret_cast<const uint4 *>(P.chunk + c0 + c) : make_uint4(0, 0, 0, 0);
+        const uint4 q = act ? *reinterpret_cast<const uint4 *>(P.lchunk + c0 + c) : make_uint4(0, 0, 0, 0);
         const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
         uint32_t first = 4;
 #pragma unroll
@@ -1010,8 +462,8 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t cbase
         if (!ballot(has && !found && it + 64 < nch)) break;
     }
     // the break chunk's ops (row lanes 0-7) and the walk position before it (row lane 8)
-    const uint32_t w = has && t < CHUNK ? P.cigar[op0 + (uint64_t)bc * CHUNK + (uint32_t)t] : 0u;
-    const uint32_t pv = has && t == CHUNK ? (bc ? P.chunk[c0 + bc - 1] & CH_POS : rpos) : 0u;
+    const uint32_t w = has && t < CHUNK ? P.lcig[op0 + (uint64_t)bc * CHUNK + (uint32_t)t] : 0u;
+    const uint32_t pv = has && t == CHUNK ? (bc ? P.lchunk[c0 + bc - 1] & CH_POS : rpos) : 0u;
     const uint32_t before = (uint32_t)__shfl((int)pv, 16 * g + CHUNK, WAVE);
     uint32_t x = t < CHUNK ? ref_adv(w) : 0u;
     x += dpp<0x111, 0xf>(x);   // inclusive row scan
@@ -1025,116 +477,6 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t cbase
     return m;
 }
 
-template <int KIND, bool COUNT>
-__device__ __forceinline__ void gather_event(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
-                                             WinStats &st) {
-    // Walk positions of index-walked reads are < 2^29 (the others are flagged slow at load
-    // time); windows ending at or past 2^31 take the exact per-read path.
-    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
-    const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
-    int64_t lo, hi;
-    if (!read_range(P, tid, beg, end, lo, hi, COUNT ? &st : nullptr)) return;
-#if SVT_DIAG == 1
-    if (lo < hi) return;     // diagnostic build: region query only
-#endif
-    const int ln = lane_id();
-    uint32_t live_ops = 0;   // COUNT builds
-    // the contig's first arena offset (stop_rows' reads' offsets from their rec.w)
-    const uint64_t cbase = KIND == K_END ? P.off64[P.tid_off[tid]] : 0ull;
-    for (int64_t rb = lo; rb < hi; rb += WAVE) {
-        const int64_t r = rb + ln;
-        const bool inb = r < hi;
-        const uint4 rc = inb ? P.rec[r] : make_uint4(0, 0, 0, 0);
-        const uint4 r2 = inb ? P.rec2[r] : make_uint4(0, 0, 0, 0);
-        const uint32_t rpos = rc.x, ncig = rc.z & NCIG_MASK, clip = rc.z >> 30;
-        const bool slow = (rc.z & SLOW_BIT) != 0;
-        const bool ovl = inb && (int64_t)(int32_t)rc.y > beg;      // hts_itr_next overlap; pos < end below hi
-        const bool live = ovl && !slow && ncig > 0;
-        const uint32_t wend = r2.x;                                 // walk position after the last op
-        const bool brk = wend > e;                                  // refinement.c:145 fires somewhere
-        // reads with n_cigar == 0: the loop body never runs, only the soft-clip tests do
-        if (KIND != K_INS) {
-            const bool z = ovl && ncig == 0 && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
-            if (KIND == K_START) sink.push(z && (clip & SVT_CLIP_LAST_S), (int32_t)rpos);       // :152
-            else sink.push(z && (clip & SVT_CLIP_FIRST_S), (int32_t)(rpos + 1u));                // :210-220
-        }
-        if (COUNT) {
-            st.reads += (unsigned long long)__popcll(ballot(ovl && !slow));
-            if (KIND != K_INS) st.ops += (unsigned long long)__popcll(ballot(ovl && ncig == 0));
-            st.range += (unsigned long long)__popcll(ballot(inb));
-        }
-        // candidate ops processed before the break (refinement.c:124-136 / :190-200 / :299-310)
-        {
-            uint32_t n = live ? r2.y : 0u;
-            const uint32_t n_list = n;
-            // the first one is inline in rec2 (most reads carry at most one)
-            auto take = [&](uint2 a, uint32_t k) {
-                if (a.x > e) n = k;
-                else if (is_candidate_op<KIND>(a.y & 0xfu, a.y >> 4))
-                    sink.push1(KIND == K_END ? (int32_t)(a.x + (a.y >> 4) + 1u) : (int32_t)a.x);
-            };
-            if (n > 0) take(make_uint2(r2.z, r2.w), 0);
-            if (ballot(n > 1)) {
-                const uint2 *evp = P.ev + (n > 1 ? P.evoff[r] : 0ull);
-                uint2 a = n > 1 ? evp[1] : make_uint2(0, 0), b = n > 2 ? evp[2] : make_uint2(0, 0);
-                for (uint32_t k = 1; ballot(k < n); k += 2) {
-                    if (k < n) take(a, k);
-                    if (k + 1 < n) take(b, k + 1);
-                    a = k + 2 < n ? evp[k + 2] : make_uint2(0, 0);
-                    b = k + 3 < n ? evp[k + 3] : make_uint2(0, 0);
-                }
-            }
-            if (COUNT) {   // entries needed past the inline one: up to the first past inter.end
-                const uint32_t need = n_list ? min(n, n_list - 1u) : 0u;
-                st.lreads += (unsigned long long)__popcll(ballot(need > 0));
-                uint32_t tot = need;
-#pragma unroll
-                for (int d = 32; d > 0; d >>= 1) tot += (uint32_t)__shfl_xor((int)tot, d, WAVE);
-                st.lentries += tot;
-            }
-        }
-        // soft-clip candidates at the walk's stop
-        if (KIND == K_START)   // trailing S, no break, s <= rp <= e  (refinement.c:147-159)
-            sink.push(live && !brk && (clip & SVT_CLIP_LAST_S) && s <= wend, (int32_t)wend);
-        if (KIND == K_END) {   // leading S, s <= pos <= e: walked rp + 1  (refinement.c:210-220)
-            const bool stop = live && (clip & SVT_CLIP_FIRST_S) && (int64_t)s <= (int64_t)rpos && (int64_t)rpos <= (int64_t)e;
-            sink.push(stop && !brk, (int32_t)(wend + 1u));
-            uint64_t m = COUNT || SVT_DIAG == 3 ? 0ull : ballot(stop && brk);
-            while (m) m = stop_rows(P, cbase, m, ncig, rpos, rc.w, e, sink);
-        }
-        if (COUNT) {   // ops walked: every op up to the break op, or all ops; + the soft-clip test word
-            uint64_t m = ballot(live);
-            while (m) {
-                const int l = __builtin_ctzll(m);
-                m &= m - 1;
-                const uint32_t nc = rdlane(ncig, l), rp = rdlane(rpos, l);
-                const bool bl = rdlane(wend, l) > e;
-                uint32_t walked = nc;
-                if (bl) {
-                    uint32_t bi;
-                    const uint32_t aft = break_after(P, P.off64[rb + l], nc, rp, e, bi);
-                    walked = bi + 1;
-                    if (KIND == K_END && (rdlane(clip, l) & SVT_CLIP_FIRST_S) && s <= rp && rp <= e) {
-                        if (ln == 0) sink.push1((int32_t)(aft + 1u));
-                        st.stops++;                                   // stop_rows' search for this read:
-                        st.stopch += (unsigned long long)(bi / CHUNK + 1u);   // chunk words to the break chunk
-                    }
-                    if (KIND == K_START && bi + 1 != nc) walked++;   // cigar[n-1] test word
-                }
-                if (ln == 0) live_ops += walked;
-            }
-        }
-        // reads whose walk could leave the index's range: exact per-read replay
-        uint64_t sm = ballot(ovl && slow);
-        while (sm) {
-            const int l = __builtin_ctzll(sm);
-            sm &= sm - 1;
-            walk_read<KIND, COUNT>(P.cigar, P.off64[rb + l], rdlane(ncig, l), rdlane(rpos, l), rdlane(clip, l), s, e,
-                                   sink, st);
-        }
-    }
-    if (COUNT) st.ops += rdlane(live_ops, 0);
-}
 
 // ------------------------------------------------------------------ span walk (default)
 // The reads [lo, hi) of a window own one contiguous span of the D (or I) event list, and
@@ -1165,7 +507,6 @@ __device__ __forceinline__ void span_count(const DevPileup &P, int tid, uint32_t
     st.squeries++;
     st.span += E1 - E0;
     if (KIND != K_END) return;
-    const uint64_t cbase = P.off64[P.tid_off[tid]];
     for (uint64_t b = E0; b < E1; b += WAVE) {
         const uint64_t j = b + (uint64_t)lane_id();
         const uint4 v = j < E1 ? ev[j] : make_uint4(0, 0, 0, 0);
@@ -1175,9 +516,8 @@ __device__ __forceinline__ void span_count(const DevPileup &P, int tid, uint32_t
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1;
-            const uint32_t offlo = rdlane(v.w, l);
             uint32_t bi;
-            (void)break_after(P, cbase + (uint64_t)(offlo - (uint32_t)cbase), NCIG_MASK, rdlane(v.x, l), e, bi);
+            (void)break_after(P, (uint64_t)rdlane(v.w, l) * ALIGN_OPS, NCIG_MASK, rdlane(v.x, l), e, bi);
             st.stops++;
             st.stopch += (unsigned long long)(bi / CHUNK + 1u);
         }
@@ -1269,13 +609,11 @@ __device__ __forceinline__ bool span_cand(const uint4 &v, uint32_t s, uint32_t e
 template <int KIND>
 __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t s, uint32_t e, int64_t lo, int64_t hi,
                                           uint64_t E0, uint64_t E1, uint64_t nslow, Sink &sink,
-                                          uint64_t cbase_in = ~0ull, const StopList *defer = nullptr) {
+                                          const StopList *defer = nullptr) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u);
     const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);   // read_range yielded reads: beg < end <= 2^31 - 1
     const int ln = lane_id();
     const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
-    // the stop searches' arena base: the contig's first arena offset (given, or loaded here)
-    const uint64_t cbase = KIND != K_END ? 0ull : cbase_in != ~0ull ? cbase_in : P.off64[P.tid_off[tid]];
     int32_t cnt = 0;   // candidates appended so far (wave-uniform)
     for (uint64_t b = E0; b < E1; b += SPAN_U * WAVE) {
         uint4 v[SPAN_U];
@@ -1307,13 +645,12 @@ __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t 
                     base = rdlane_i(base, 0);
                     const int32_t qi = base + (int32_t)mbcnt(sm);
                     if (brk && qi < defer->cap) {
-                        const uint64_t op0 = cbase + (uint64_t)(v[u].w - (uint32_t)cbase);
-                        defer->q[qi] = StopReq{(uint32_t)(op0 / ALIGN_OPS), x, e, defer->kw};
+                        defer->q[qi] = StopReq{v[u].w, x, e, defer->kw};
                     }
                 } else if (sm) {   // the position after the break op, rare: the sink's LDS counter takes over
                     if (ln == 0) *sink.cnt = cnt;
                     wave_sync();
-                    while (sm) sm = stop_rows(P, cbase, sm, NCIG_MASK, x, v[u].w, e, sink);
+                    while (sm) sm = stop_rows(P, sm, NCIG_MASK, x, v[u].w, e, sink);
                     wave_sync();
                     cnt = uniform_i(*sink.cnt);
                 }
@@ -1815,27 +1152,24 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
 }
 
 struct WinLds {
-    union {                       // the gather scratch is dead once the vote starts
-        StreamLds sl;
-        IndexLds il;
-        int64_t pre[CAP + 1];
-    };
+    int64_t pre[CAP + 1];         // the wave-wide vote's prefix sums
     int32_t cand[CAP];
     int32_t ncand;
 };
 
-constexpr int G_PERREAD = 0, G_STREAM = 1, G_INDEX = 2, G_EVENT = 3, G_SPAN = 4;   // window gather variants (SVTREK_GATHER)
+// The window gather: the span walk (gather_span).  Round 1-2's A/B variants (per-read, CIGAR
+// stream, chunk index, candidate-op lists) are retired; G stays a template parameter of the
+// wave-wide window path so that diagnostic builds can plug a gather in.
+constexpr int G_SPAN = 4;
 
 template <int KIND, bool COUNT, int G>
 __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, uint32_t e, Sink &sink, WinStats &st,
                                           WinLds &L) {
     if (lane_id() == 0) *sink.cnt = 0;
     wave_sync();
-    if (G == G_SPAN) gather_span<KIND, COUNT>(a.pile, tid, s, e, sink, st);
-    else if (G == G_EVENT) gather_event<KIND, COUNT>(a.pile, tid, s, e, sink, st);
-    else if (G == G_INDEX) gather_index<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.il);
-    else if (G == G_STREAM) gather_stream<KIND, COUNT>(a.pile, tid, s, e, sink, st, L.sl);
-    else gather_perread<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    static_assert(G == G_SPAN, "span walk only");
+    (void)L;
+    gather_span<KIND, COUNT>(a.pile, tid, s, e, sink, st);
     wave_sync();
     return uniform_i(*sink.cnt);
 }
@@ -1950,8 +1284,6 @@ __device__ __forceinline__ void refine_body(const KArgs &a);
 template <bool COUNT, int G>
 __global__ __launch_bounds__(64 * WPB) void refine_kernel(KArgs a) { refine_body<COUNT, G>(a); }
 
-__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_index_kernel(KArgs a) { refine_body<false, G_INDEX>(a); }
-__global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_event_kernel(KArgs a) { refine_body<false, G_EVENT>(a); }
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_span_kernel(KArgs a) { refine_body<false, G_SPAN>(a); }
 
 __device__ __forceinline__ void write_result(const KArgs &a, uint32_t li, uint32_t w, uint32_t r) {
@@ -2133,7 +1465,7 @@ constexpr int LW_U = SVT_LW_U;   // 64-event slots per step of lane_walk (loads 
 
 template <int KIND>
 __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
-                                              int32_t lo, int32_t hi, uint16_t *row, uint64_t cbase,
+                                              int32_t lo, int32_t hi, uint16_t *row,
                                               LaneStops &defer) {
     const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);
     const int ln = lane_id();
@@ -2171,8 +1503,7 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
                     const int32_t qi = defer.n + (int32_t)mbcnt(brk);
                     defer.n += (int32_t)__popcll(brk);
                     if (__builtin_amdgcn_inverse_ballot_w64(brk) && qi < LV_STOPS) {
-                        const uint64_t op0 = cbase + (uint64_t)(v[u].w - (uint32_t)cbase);
-                        defer.q[qi] = StopReq{(uint32_t)(op0 / ALIGN_OPS), v[u].x, e, defer.kw};
+                        defer.q[qi] = StopReq{v[u].w, v[u].x, e, defer.kw};
                     }
                 }
             }
@@ -2299,7 +1630,7 @@ __device__ __forceinline__ uint32_t stop_lane(const DevPileup &P, const StopReq 
     const uint64_t op0 = (uint64_t)r.op32 * ALIGN_OPS, c0 = op0 / CHUNK;
     uint32_t prev = r.rpos, bc = 0, before = r.rpos;
     for (uint32_t c = 0;; c += 4) {   // the break exists (walk end > e): the scan ends inside the read
-        const uint4 q = *reinterpret_cast<const uint4 *>(P.chunk + c0 + c);
+        const uint4 q = *reinterpret_cast<const uint4 *>(P.lchunk + c0 + c);
         const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
         int f = 4;
 #pragma unroll
@@ -2312,7 +1643,7 @@ __device__ __forceinline__ uint32_t stop_lane(const DevPileup &P, const StopReq 
         }
         prev = E[3];
     }
-    const uint4 *cw = reinterpret_cast<const uint4 *>(P.cigar + op0 + (uint64_t)bc * CHUNK);
+    const uint4 *cw = reinterpret_cast<const uint4 *>(P.lcig + op0 + (uint64_t)bc * CHUNK);
     const uint4 w0 = cw[0], w1 = cw[1];
     const uint32_t W[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
     uint32_t after = before, res = 0;
@@ -2332,7 +1663,7 @@ struct LvQuery {
     int32_t kind;          // K_* (| LQ_REDO), -1: no window (NA)
     int32_t lo;            // the vote's band low end: pos - (range + max(ci, 0))
     uint32_t s, e, liw, len;        // the window, li << 1 | w, its span's event count
-    uint32_t e0[2], cb[2];          // the span's first event, the contig's first arena offset
+    uint32_t e0[2];                 // the span's first event
 };
 static_assert(sizeof(LvQuery) <= LV_S * 2, "LvQuery must fit a staging row");
 
@@ -2380,10 +1711,8 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
     const uint64_t E0 = off[lo], E1 = off[hi];
     // slow reads: exact per-read replay; spans of 2^31 events or more: the wave-wide path
     if (P.slowpre[hi] != P.slowpre[lo] || E1 - E0 >= 0x80000000ull) { q.kind |= LQ_REDO; return; }
-    const uint64_t cb = q.kind == K_END ? P.off64[ra] : 0ull;
     q.e0[0] = (uint32_t)E0; q.e0[1] = (uint32_t)(E0 >> 32);
     q.len = (uint32_t)(E1 - E0);
-    q.cb[0] = (uint32_t)cb; q.cb[1] = (uint32_t)(cb >> 32);
 }
 
 template <int LV_W>
@@ -2413,7 +1742,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
         if ((uint32_t)ln < cnt) {
             const LvQuery q = *reinterpret_cast<const LvQuery *>(L.stage + (uint32_t)ln * LV_S);
-            write_result(a, q.liw >> 1, q.liw & 1u, (uint32_t)q.kind ^ q.e0[0] ^ q.len ^ q.cb[0]);
+            write_result(a, q.liw >> 1, q.liw & 1u, (uint32_t)q.kind ^ q.e0[0] ^ q.len);
         }
         return;
     }
@@ -2427,8 +1756,6 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         const uint32_t len = (uint32_t)uniform_i((int32_t)qp->len);
         const uint64_t E0 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[0]) |
                             (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[1]) << 32;
-        const uint64_t cb = (uint64_t)(uint32_t)uniform_i((int32_t)qp->cb[0]) |
-                            (uint64_t)(uint32_t)uniform_i((int32_t)qp->cb[1]) << 32;
         wave_sync();   // the row may be overwritten from here on
         uint32_t flags = 0;
         int32_t n = 0;
@@ -2442,9 +1769,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             LaneBand r{0, 0, 0u};
             uint16_t *row = L.stage + kw * LV_S;
             if (len) {
-                if (qk == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, cb, stops);
-                else if (qk == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, cb, stops);
-                else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, cb, stops);
+                if (qk == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, stops);
+                else if (qk == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, stops);
+                else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, stops);
             }
             flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : stops.n > LV_STOPS ? LV_REDO | LV_WHY(4)
                                                                             : (uint32_t)r.nb | LV_PENDING | r.flags;
@@ -2610,166 +1937,7 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
     best[q] = b;
 }
 
-// svt_load_pileup's per-op work, on the device: one wave per read copies the read's
-// CIGAR words from the caller's unpadded layout into the padded arena (coalesced), and
-// builds the read's chunk index: for every CHUNK ops (zero padding up to ALIGN_OPS
-// included; a read with n_cigar == 0 still owns one padded lane group) the reference walk
-// position after the chunk (refinement.c:141, a wave prefix scan carried across 64-op
-// steps), the DEL/INS candidate flags and, on the read's first chunk, CH_HEAD.  Reads whose
-// walk reaches 2^29 (the chunk word's range) are flagged SLOW_BIT: those take walk_read's
-// exact uint32 replay.  The host only does per-read work (offsets, prefix-max, buckets).
-__global__ __launch_bounds__(256) void pack_kernel(const uint32_t *__restrict__ raw, const uint64_t *__restrict__ raw_off,
-                                                   const uint64_t *__restrict__ poff, uint4 *rec,
-                                                   uint32_t *__restrict__ arena, uint32_t *__restrict__ chunk,
-                                                   uint4 *__restrict__ rec2, uint64_t *__restrict__ cnt, int64_t S,
-                                                   int64_t nr) {
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= nr) return;
-    const int ln = lane_id();
-    const uint64_t o0 = raw_off[r], n = raw_off[r + 1] - o0, dst = poff[r];
-    const uint64_t npad = n ? (n + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1) : (uint64_t)ALIGN_OPS;
-    const uint32_t rpos = rec[r].x;
-    uint64_t walk = 0;
-    uint32_t carry = rpos, nev = 0, nins = 0;
-    // PK_U 64-op steps per pass: their words are loaded up front (PK_U loads in flight per
-    // wave instead of one), then scanned in order
-    constexpr int PK_U = 8;
-    for (uint64_t b0 = 0; b0 < npad; b0 += PK_U * WAVE) {
-        uint32_t wv[PK_U];
-#pragma unroll
-        for (int u = 0; u < PK_U; u++) {
-            const uint64_t i = b0 + (uint64_t)(u * WAVE + ln);
-            wv[u] = i < n ? raw[o0 + i] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < PK_U; u++) {
-            const uint64_t i0 = b0 + (uint64_t)(u * WAVE);
-            if (i0 >= npad) break;
-            const uint64_t i = i0 + (uint64_t)ln;
-            const uint32_t w = wv[u];
-            if (i < n) arena[dst + i] = w;
-            const uint32_t adv = ref_adv(w);
-            walk += adv;
-            const uint32_t after = carry + wave_scan_add(adv);
-            const uint64_t dm = ballot(is_candidate_op<K_START>(w & 0xfu, w >> 4));
-            const uint64_t im = ballot(is_candidate_op<K_INS>(w & 0xfu, w >> 4));
-            if ((ln & (CHUNK - 1)) == CHUNK - 1 && i < npad) {
-                const int sh = ln & ~(CHUNK - 1);
-                chunk[(dst + i0) / CHUNK + (uint64_t)(ln / CHUNK)] =
-                    (after & CH_POS) | (i0 == 0 && sh == 0 ? CH_HEAD : 0u) | (((dm >> sh) & 0xffull) ? CH_DEL : 0u) |
-                    (((im >> sh) & 0xffull) ? CH_INS : 0u);
-            }
-            carry = rdlane(after, WAVE - 1);
-            nev += (uint32_t)__popcll(dm | im);
-            nins += (uint32_t)__popcll(im);
-        }
-    }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) walk += __shfl_xor(walk, d, WAVE);
-    if (ln == 0) {
-        const uint32_t z = rec[r].z;
-        const bool slow = (uint64_t)rpos + walk >= INDEX_LIMIT || walk >= WALK_LIMIT;
-        if (slow) rec[r].z = z | SLOW_BIT;
-        rec2[r] = make_uint4(rpos + (uint32_t)walk, nev, 0u, 0u);
-        // per-read counts, one array of stride S = n_reads + 1 each (exclusive scans -> offsets)
-        cnt[r] = nev;                                  // candidate ops (D > 50 or I >= 50): event lists
-        cnt[S + r] = nins;                             // I >= 50 ops (allele-consensus sequences, svt_load_insseq)
-        cnt[2 * S + r] = slow ? 0u : nev - nins + (uint32_t)__popc(z >> 30);   // span D list (+ soft-clip events)
-        cnt[3 * S + r] = slow ? 0u : nins;                                    // span I list
-        cnt[4 * S + r] = slow ? 1u : 0u;                                     // slow reads (exact per-read walk)
-    }
-}
-
-// Span events of every read (see SP_TRAIL / SP_LEAD): its D list at spoffD[r], I list at
-// spoffI[r], candidate ops in op order with the walk position before each (refinement.c:141).
-// Slow reads own no events (pack_kernel counted none for them).
-__global__ __launch_bounds__(256) void span_kernel(const uint32_t *__restrict__ arena, const uint64_t *__restrict__ poff,
-                                                   const uint4 *__restrict__ rec, const uint4 *__restrict__ rec2,
-                                                   const uint64_t *__restrict__ spoffD, const uint64_t *__restrict__ spoffI,
-                                                   uint4 *__restrict__ spD, uint4 *__restrict__ spI, int64_t nr) {
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= nr) return;
-    const int ln = lane_id();
-    uint64_t kD = spoffD[r], kI = spoffI[r];
-    if (spoffD[r + 1] == kD && spoffI[r + 1] == kI) return;
-    const uint4 rc = rec[r];
-    const uint64_t n = rc.z & NCIG_MASK, src = poff[r];
-    const uint32_t clip = rc.z >> 30, rpos = rc.x, endp = rc.y, wend = rec2[r].x;
-    if (clip & SVT_CLIP_FIRST_S) {   // refinement.c:210-220: cigar[0] == S
-        if (ln == 0) spD[kD] = make_uint4(rpos, ((wend - rpos) << 4) | SP_LEAD, endp, (uint32_t)src);
-        kD++;
-    }
-    uint32_t carry = rpos;
-    constexpr int SP_UN = 4;   // as pack_kernel: SP_UN loads in flight per wave
-    for (uint64_t b0 = 0; b0 < n; b0 += SP_UN * WAVE) {
-        uint32_t wv[SP_UN];
-#pragma unroll
-        for (int u = 0; u < SP_UN; u++) {
-            const uint64_t i = b0 + (uint64_t)(u * WAVE + ln);
-            wv[u] = i < n ? arena[src + i] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < SP_UN; u++) {
-            if (b0 + (uint64_t)(u * WAVE) >= n) break;
-            const uint32_t w = wv[u];
-            const uint32_t adv = ref_adv(w);
-            const uint32_t after = carry + wave_scan_add(adv);
-            const bool d = is_candidate_op<K_START>(w & 0xfu, w >> 4), ins = is_candidate_op<K_INS>(w & 0xfu, w >> 4);
-            const uint64_t md = ballot(d), mi = ballot(ins);
-            const uint4 ev = make_uint4(after - adv, w, endp, 0u);
-            if (d) spD[kD + mbcnt(md)] = ev;
-            if (ins) spI[kI + mbcnt(mi)] = ev;
-            kD += (uint64_t)__popcll(md);
-            kI += (uint64_t)__popcll(mi);
-            carry = rdlane(after, WAVE - 1);
-        }
-    }
-    if ((clip & SVT_CLIP_LAST_S) && ln == 0) spD[kD] = make_uint4(wend, SP_TRAIL, endp, 0u);   // :120,:147-159
-}
-
-// Second load pass: every read's candidate ops (D > 50 or I >= 50, refinement.c:124,:190,:299)
-// with the walk position before each (refinement.c:141), in op order, at the read's event
-// offset (an exclusive scan of pack_kernel's counts).
-__global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__ arena, const uint64_t *__restrict__ poff,
-                                                    const uint4 *__restrict__ rec, uint4 *__restrict__ rec2,
-                                                    const uint64_t *__restrict__ evoff, uint2 *__restrict__ ev,
-                                                    int64_t nr) {
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= nr) return;
-    const int ln = lane_id();
-    const uint4 rc = rec[r];
-    const uint64_t n = rc.z & NCIG_MASK, src = poff[r], o0 = evoff[r];
-    if (evoff[r + 1] == o0) return;
-    uint32_t carry = rc.x;
-    uint64_t k = o0;
-    constexpr int EV_U = 4;   // as pack_kernel: EV_U loads in flight per wave
-    for (uint64_t b0 = 0; b0 < n; b0 += EV_U * WAVE) {
-        uint32_t wv[EV_U];
-#pragma unroll
-        for (int u = 0; u < EV_U; u++) {
-            const uint64_t i = b0 + (uint64_t)(u * WAVE + ln);
-            wv[u] = i < n ? arena[src + i] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < EV_U; u++) {
-            if (b0 + (uint64_t)(u * WAVE) >= n) break;
-            const uint32_t w = wv[u];
-            const uint32_t adv = ref_adv(w);
-            const uint32_t after = carry + wave_scan_add(adv);
-            const bool c = is_candidate_op<K_START>(w & 0xfu, w >> 4) || is_candidate_op<K_INS>(w & 0xfu, w >> 4);
-            const uint64_t m = ballot(c);
-            if (c) {
-                const uint32_t rank =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                ev[k + rank] = make_uint2(after - adv, w);
-                if (k + rank == o0) rec2[r].z = after - adv, rec2[r].w = w;   // the first one, inline
-            }
-            k += (uint64_t)__popcll(m);
-            carry = rdlane(after, WAVE - 1);
-        }
-    }
-}
-
+#include "svt_index.inc"
 #include "svt_poa.inc"
 
 }  // namespace
@@ -2778,11 +1946,11 @@ __global__ __launch_bounds__(256) void event_kernel(const uint32_t *__restrict__
 struct svt_ctx {
     svt_params prm{};
     int device = 0;
-    int gather = G_SPAN;          // SVTREK_GATHER=event / index / stream / perread select the A/B variants
-    bool lane_vote = true;        // span: refine_lane_kernel; SVTREK_GATHER=span1: refine_span_kernel
+    bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
     int lane_w = 0;               // SVTREK_LANE_W=8|32 forces the lane kernel's windows per wave (A/B)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
+    uint32_t lane_par = 0;        // which of the two redo counters the next lane launch uses
     char err[512] = {0};
     // pileup
     int32_t n_targets = 0;
@@ -2790,22 +1958,26 @@ struct svt_ctx {
     uint64_t n_ops = 0;
     int32_t *d_pos = nullptr, *d_emax = nullptr;
     uint4 *d_rec = nullptr;
-    uint64_t *d_off64 = nullptr;
+    uint64_t *d_off64 = nullptr;      // stream offsets [n_reads + 1]
     int64_t *d_tid_off = nullptr, *d_bkt_off = nullptr;
     uint2 *d_bkt = nullptr;
-    uint32_t *d_cigar = nullptr;
-    uint32_t *d_chunk = nullptr;
-    uint4 *d_rec2 = nullptr;
-    uint64_t *d_evoff = nullptr;
+    uint32_t *d_cigar = nullptr;      // CIGAR stream
+    uint2 *d_rec2 = nullptr;
     uint64_t *d_insbase = nullptr;    // per read: its first I >= 50 op's index in the insertion sequences
     uint64_t n_ins = 0;               // I >= 50 ops in the pileup
+    // device index (svt_index.inc)
+    uint64_t *d_part = nullptr;       // [n_ranges + 1]
+    uint32_t n_ranges = 0;
+    uint32_t *d_wtot = nullptr;
+    uint64_t *d_wbase = nullptr, *d_tot = nullptr;
+    uint32_t *d_lcig = nullptr, *d_lchunk = nullptr;
+    uint64_t n_evD = 0, n_evI = 0, n_slow = 0, n_lead_blocks = 0;
     // allele-consensus mode (svt_load_insseq / svt_poa_consensus)
     uint64_t *d_ins_off = nullptr;
     uint8_t *d_ins_bases = nullptr;
     bool insseq_loaded = false;
     PoaPool poa_small, poa_big;       // POA scratch slots (poa_pool)
     uint64_t poa_deferred = 0;        // loci the last svt_poa_consensus reran on full-size slots
-    uint2 *d_ev = nullptr;
     uint64_t *d_spoffD = nullptr, *d_spoffI = nullptr, *d_slowpre = nullptr;   // span walk
     uint4 *d_spD = nullptr, *d_spI = nullptr;
     uint64_t dev_bytes = 0;
@@ -2899,18 +2071,19 @@ svt_status grow_pool(svt_ctx *c) {
 
 void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
-    hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar); hfree(c->d_chunk);
-    hfree(c->d_rec2); hfree(c->d_evoff); hfree(c->d_ev); hfree(c->d_insbase); hfree(c->d_ins_off);
-    hfree(c->d_ins_bases);
+    hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
+    hfree(c->d_rec2); hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
+    hfree(c->d_part); hfree(c->d_wtot); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_lcig); hfree(c->d_lchunk);
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
-    c->insseq_loaded = false; c->n_ins = 0;
+    c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
+    c->n_evD = c->n_evI = c->n_slow = c->n_lead_blocks = 0;
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
-                       c->d_cigar, c->d_chunk, c->d_rec2, c->d_evoff, c->d_ev, c->d_spoffD, c->d_spoffI,
+                       c->d_cigar, c->d_lcig, c->d_lchunk, c->d_rec2, c->d_spoffD, c->d_spoffI,
                        c->d_spD, c->d_spI, c->d_slowpre, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
                     c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
@@ -2943,9 +2116,8 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     // order_on); the work counters of a counting launch start from zero; the head word is
     // cleared once per epoch cycle
     c->epoch = c->epoch % ((1u << 24) - 1u) + 1u;
-    if (c->epoch == 1) {   // a new epoch cycle: pool head and both redo counters start from zero
+    if (c->epoch == 1) {   // a new epoch cycle: the pool head starts from zero
         HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 8, st));
-        HIP_TRY(c, hipMemsetAsync(c->d_ctl + CTL_REDO, 0, 8, st));
     }
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_ctl + 16, 0, 8 * W_N, st));
     KArgs a = make_args(c, d_loci, d_out, (uint32_t)n, count);
@@ -2953,47 +2125,36 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     a.rec_index = rec_index;
     a.rec_base = rec_base;
     dim3 grid((unsigned)((2 * n + WPB - 1) / WPB)), block(64 * WPB);
-    if (c->gather == G_SPAN) {
-        if (count) hipLaunchKernelGGL((refine_kernel<true, G_SPAN>), grid, block, 0, st, a);
+    if (count) {
+        hipLaunchKernelGGL((refine_kernel<true, G_SPAN>), grid, block, 0, st, a);
+    } else if (c->lane_vote && (c->lane_w != 0 || 2 * n >= (size_t)65536)) {
         // lane kernel (32 windows a wave) once the batch has >= 64K windows; below that the
         // one-wave-per-window span kernel is as fast or faster (fewer, longer waves leave the
         // chip underfilled: cfg2 20K windows 33 us span vs 76 us lane<8>, 107 us lane<32>;
         // cfg3 100K windows 111 vs 109 us; cfg4 2M windows 2.23 ms vs 0.905 ms)
-        else if (c->lane_vote && (c->lane_w != 0 || 2 * n >= (size_t)65536)) {
-            if (c->redo_cap < 2 * n) {   // window list of the wave-wide left-overs (grown, never shrunk)
-                hfree(c->d_redo);
-                c->redo_cap = 0;
-                HIP_TRY(c, hipMalloc(&c->d_redo, 2 * n * sizeof(uint32_t)));
-                c->redo_cap = 2 * n;
-            }
-            a.redo_list = c->d_redo;
-            a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->epoch & 1u);
-            a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + ((c->epoch + 1u) & 1u);
-            if (c->lane_w == 8)
-                hipLaunchKernelGGL(refine_lane_kernel<8>, dim3((unsigned)((2 * n + WPB * 8 - 1) / (WPB * 8))), block, 0,
-                                   st, a);
-            else
-                hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
-                                   st, a);
-            hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
-        } else {
-            // the redo kernel of a lane launch zeroes the next epoch's counter; without one, do it here
-            if (c->lane_vote)
-                HIP_TRY(c, hipMemsetAsync(c->d_ctl + CTL_REDO + 4u * ((c->epoch + 1u) & 1u), 0, 4, st));
-            hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
+        if (c->redo_cap < 2 * n) {   // window list of the wave-wide left-overs (grown, never shrunk)
+            hfree(c->d_redo);
+            c->redo_cap = 0;
+            HIP_TRY(c, hipMalloc(&c->d_redo, 2 * n * sizeof(uint32_t)));
+            c->redo_cap = 2 * n;
         }
-    } else if (c->gather == G_EVENT) {
-        if (count) hipLaunchKernelGGL((refine_kernel<true, G_EVENT>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL(refine_event_kernel, grid, block, 0, st, a);
-    } else if (c->gather == G_INDEX) {
-        if (count) hipLaunchKernelGGL((refine_kernel<true, G_INDEX>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL(refine_index_kernel, grid, block, 0, st, a);
-    } else if (c->gather == G_STREAM) {
-        if (count) hipLaunchKernelGGL((refine_kernel<true, G_STREAM>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((refine_kernel<false, G_STREAM>), grid, block, 0, st, a);
+        // Two left-over counters alternate between lane launches: this launch appends to
+        // ctr[par]; its redo kernel reads that and zeroes ctr[par ^ 1] for the next lane launch.
+        // The parity advances on lane launches only (counting and span launches in between
+        // leave both counters alone), and both start zeroed (svt_open).
+        a.redo_list = c->d_redo;
+        a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + c->lane_par;
+        a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->lane_par ^ 1u);
+        c->lane_par ^= 1u;
+        if (c->lane_w == 8)
+            hipLaunchKernelGGL(refine_lane_kernel<8>, dim3((unsigned)((2 * n + WPB * 8 - 1) / (WPB * 8))), block, 0,
+                               st, a);
+        else
+            hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
+                               st, a);
+        hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
     } else {
-        if (count) hipLaunchKernelGGL((refine_kernel<true, G_PERREAD>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((refine_kernel<false, G_PERREAD>), grid, block, 0, st, a);
+        hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
     }
     HIP_TRY(c, hipGetLastError());
     return SVT_OK;
@@ -3176,13 +2337,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     svt_ctx *c = new (std::nothrow) svt_ctx();
     if (!c) return SVT_ENOMEM;
     c->prm = *params;
-    const char *g = getenv("SVTREK_GATHER");
-    c->gather = !g ? G_SPAN
-                : strcmp(g, "perread") == 0 ? G_PERREAD
-                : strcmp(g, "stream") == 0  ? G_STREAM
-                : strcmp(g, "index") == 0   ? G_INDEX
-                : strcmp(g, "event") == 0   ? G_EVENT
-                                            : G_SPAN;
+    const char *g = getenv("SVTREK_GATHER");   // "span1": the one-wave-per-window kernel at every batch size
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
@@ -3209,7 +2364,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     // load the code object now (HIP loads it lazily at the first launch), so that no later
     // call -- and no timing of one -- pays for it
     hipFuncAttributes fa;
-    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(pack_kernel));
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(index_kernel<false>));
     *out = c;
     return SVT_OK;
 }
@@ -3235,6 +2390,103 @@ svt_status svt_open_multi(const svt_params *params, int device_count, const int 
 
 int svt_device_count(const svt_ctx *c) { return c ? 1 + (int)c->subs.size() : 0; }
 
+extern "C++" {
+namespace {
+
+// Run fn(k) for k = 0 .. n-1 on up to `cap` threads (the host pass of svt_load_pileup is per contig).
+template <typename F>
+void parallel_for(size_t n, size_t cap, F fn) {
+    const size_t T = std::max<size_t>(1, std::min<size_t>({n, cap, (size_t)std::max(1u, std::thread::hardware_concurrency())}));
+    if (T <= 1) {
+        for (size_t k = 0; k < n; k++) fn(k);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; t++)
+        th.emplace_back([&] {
+            for (size_t k; (k = next.fetch_add(1)) < n;) fn(k);
+        });
+    for (auto &x : th) x.join();
+}
+
+// The device index of the loaded pileup (svt_index.inc): census, scan of the range totals, emit.
+// `first`: size and allocate the event lists and the lead arena from the totals (one synchronous
+// read-back); later calls (svt_reindex) reuse them -- the totals depend on the pileup only.
+// `ms`: the index kernels' device time (HIP events; the read-back and allocations excluded).
+svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
+    IxArgs a;
+    a.stream = c->d_cigar;
+    a.soff = c->d_off64;
+    a.rec = c->d_rec;
+    a.rec2 = c->d_rec2;
+    a.part = c->d_part;
+    a.wtot = c->d_wtot;
+    a.wbase = c->d_wbase;
+    a.spoffD = c->d_spoffD;
+    a.spoffI = c->d_spoffI;
+    a.insbase = c->d_insbase;
+    a.slowpre = c->d_slowpre;
+    a.n_ranges = c->n_ranges;
+    const dim3 grid((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block(64 * IX_WPB);
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (ms)
+        for (auto &e : ev) HIP_TRY(c, hipEventCreate(&e));
+    auto done = [&](svt_status r) {
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        return r;
+    };
+    if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
+    hipLaunchKernelGGL(index_kernel<false>, grid, block, 0, st, a);
+    hipLaunchKernelGGL(range_scan_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t *)c->d_wtot, c->d_wbase,
+                       c->n_ranges, c->d_tot, c->d_spoffD, c->d_spoffI, c->d_insbase, c->d_slowpre,
+                       (uint64_t)c->n_reads);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index census: %s", hipGetErrorString(e)));
+    if (ms && hipEventRecord(ev[1], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
+    if (first) {
+        uint64_t t[IX_NTOT];
+        e = hipMemcpyAsync(t, c->d_tot, sizeof t, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index totals: %s", hipGetErrorString(e)));
+        c->n_evD = t[IX_D];
+        c->n_evI = t[IX_I];
+        c->n_ins = t[IX_INS];
+        c->n_slow = t[IX_SLOW];
+        c->n_lead_blocks = t[IX_LB];
+        if (c->n_lead_blocks >= (1ull << 32))   // a lead event's block index is 32 bits
+            return done(fail(c, SVT_EINVAL, "pileup: %s", ">= 2^32 lead arena blocks (2^37 leading-S CIGAR ops)"));
+        const uint64_t lw = c->n_lead_blocks * ALIGN_OPS + LEAD_PAD, cw = c->n_lead_blocks * (ALIGN_OPS / CHUNK) + LEAD_PAD;
+        svt_status s;
+        if ((s = upload<uint4>(c, c->d_spD, nullptr, 0, std::max<uint64_t>(c->n_evD, 1)))) return done(s);
+        if ((s = upload<uint4>(c, c->d_spI, nullptr, 0, std::max<uint64_t>(c->n_evI, 1)))) return done(s);
+        if ((s = upload<uint32_t>(c, c->d_lcig, nullptr, 0, lw))) return done(s);
+        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, cw))) return done(s);
+    }
+    a.spD = c->d_spD;
+    a.spI = c->d_spI;
+    a.lcig = c->d_lcig;
+    a.lchunk = c->d_lchunk;
+    if (ms && hipEventRecord(ev[2], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
+    hipLaunchKernelGGL(index_kernel<true>, grid, block, 0, st, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index emit: %s", hipGetErrorString(e)));
+    if (ms) {
+        float t0 = 0.f, t1 = 0.f;
+        e = hipEventRecord(ev[3], st);
+        if (e == hipSuccess) e = hipEventSynchronize(ev[3]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&t0, ev[0], ev[1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&t1, ev[2], ev[3]);
+        if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index timing: %s", hipGetErrorString(e)));
+        *ms = (double)t0 + (double)t1;
+    }
+    return done(SVT_OK);
+}
+
+}  // namespace
+}  // extern "C++"
+
 static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if (!c || !p) return SVT_EINVAL;
     if (p->n_targets < 0 || (p->n_targets > 0 && !p->tid_off))
@@ -3255,174 +2507,137 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     const uint64_t nops = nr > 0 ? p->cig_off[nr] : 0;
     if (nr > 0 && p->cig_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "cig_off[0] != 0");
 
+    // ---- host pass, per contig in parallel: validation, prefix-max endpos, records, buckets
     std::vector<int32_t> emax((size_t)nr);
     std::vector<uint4> rec((size_t)nr);
-    std::vector<uint64_t> poff((size_t)nr + 1, 0);   // padded CIGAR offsets (multiples of ALIGN_OPS)
-    std::vector<int64_t> bkt_off((size_t)nt + 1, 0);
-    std::vector<uint2> bkt;
-    uint64_t pw = 0;
-    for (int32_t t = 0; t < nt; t++) {
+    std::vector<std::vector<uint2>> bk((size_t)nt);
+    std::vector<int64_t> zeros((size_t)nt, 0);   // reads with n_cigar == 0 per contig
+    std::vector<const char *> bad((size_t)nt, nullptr);
+    parallel_for((size_t)nt, 16, [&](size_t t) {
         const int64_t r0 = p->tid_off[t], r1 = p->tid_off[t + 1];
-        if (r1 - r0 > 0xffffffffll) return fail(c, SVT_EINVAL, "pileup: %s", "> 2^32 reads on one contig");
+        if (r1 - r0 > 0xffffffffll) { bad[t] = "> 2^32 reads on one contig"; return; }
         int32_t m = INT32_MIN, maxpos = 0;
+        int64_t z = 0;
         for (int64_t r = r0; r < r1; r++) {
-            if (r > r0 && p->pos[r] < p->pos[r - 1])
-                return fail(c, SVT_EINVAL, "pileup: %s", "reads not sorted by pos within a contig");
-            if (p->pos[r] < 0 || p->endpos[r] <= p->pos[r])
-                return fail(c, SVT_EINVAL, "pileup: %s", "pos < 0 or endpos <= pos");
-            uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
-            if (o1 < o0 || o1 > nops || o1 - o0 > NCIG_MASK) return fail(c, SVT_EINVAL, "pileup: %s", "bad cig_off");
-            uint32_t ncig = (uint32_t)(o1 - o0);
+            if (r > r0 && p->pos[r] < p->pos[r - 1]) { bad[t] = "reads not sorted by pos within a contig"; return; }
+            if (p->pos[r] < 0 || p->endpos[r] <= p->pos[r]) { bad[t] = "pos < 0 or endpos <= pos"; return; }
+            const uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
+            if (o1 < o0 || o1 > nops || o1 - o0 > NCIG_MASK) { bad[t] = "bad cig_off"; return; }
+            const uint32_t ncig = (uint32_t)(o1 - o0);
             uint32_t clip;
             if (p->clip) clip = p->clip[r] & 3u;
             else clip = ncig ? (((p->cigar[o1 - 1] & 0xfu) == OP_SOFT ? 1u : 0u) |
                                 ((p->cigar[o0] & 0xfu) == OP_SOFT ? 2u : 0u)) : 0u;
-            // SLOW_BIT (walk reaching 2^30) is set by pack_kernel on the device
+            z += ncig == 0;
             if (p->endpos[r] > m) m = p->endpos[r];
             maxpos = std::max(maxpos, p->pos[r]);
             emax[(size_t)r] = m;
-            poff[(size_t)r] = pw;
-            rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | (clip << 30),
-                                        (uint32_t)pw);
-            // every read, n_cigar == 0 included, owns >= 1 lane group (its head chunk)
-            pw += std::max<uint64_t>(((uint64_t)ncig + (ALIGN_OPS - 1)) & ~(uint64_t)(ALIGN_OPS - 1), ALIGN_OPS);
+            // SLOW_BIT is set by the index census on the device
+            rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | (clip << 30), 0u);
         }
-        if (r1 > r0 && pw - poff[(size_t)r0] >= (1ull << 31))
-            return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^31 CIGAR ops on one contig");
+        zeros[t] = z;
         // bucket b = 0..nb-1: {first contig-relative read with pos >= b << BKT_SHIFT, first with
         // emax >= b << BKT_SHIFT}; the last bucket lies past every pos and endpos: {nr, nr}
         const int64_t top = r1 > r0 ? std::max<int64_t>(maxpos, m) : 0;
         const int64_t nb = (top >> BKT_SHIFT) + 2;
-        bkt_off[(size_t)t] = (int64_t)bkt.size();
+        std::vector<uint2> &B = bk[t];
+        B.reserve((size_t)nb);
         int64_t rp = r0, re = r0;
         for (int64_t b = 0; b < nb; b++) {
             const int64_t x = b << BKT_SHIFT;
             while (rp < r1 && (int64_t)p->pos[rp] < x) rp++;
             while (re < r1 && (int64_t)emax[(size_t)re] < x) re++;
-            bkt.push_back(make_uint2((uint32_t)(rp - r0), (uint32_t)(re - r0)));
+            B.push_back(make_uint2((uint32_t)(rp - r0), (uint32_t)(re - r0)));
         }
+    });
+    for (int32_t t = 0; t < nt; t++)
+        if (bad[(size_t)t]) return fail(c, SVT_EINVAL, "pileup: %s", bad[(size_t)t]);
+    std::vector<int64_t> bkt_off((size_t)nt + 1, 0);
+    for (int32_t t = 0; t < nt; t++) bkt_off[(size_t)t + 1] = bkt_off[(size_t)t] + (int64_t)bk[(size_t)t].size();
+    std::vector<uint2> bkt((size_t)bkt_off[(size_t)nt]);
+    parallel_for((size_t)nt, 16, [&](size_t t) { std::copy(bk[t].begin(), bk[t].end(), bkt.begin() + bkt_off[t]); });
+    // ---- the CIGAR stream: the caller's words; a read with n_cigar == 0 gets one 0M word (no
+    // advance, never a candidate) so that every read owns a stream op (svt_index.inc)
+    int64_t nzero = 0;
+    for (int32_t t = 0; t < nt; t++) nzero += zeros[(size_t)t];
+    const uint64_t *soff = p->cig_off;
+    const uint32_t *strm = p->cigar;
+    std::vector<uint64_t> soff2;
+    std::vector<uint32_t> strm2;
+    if (nzero > 0) {
+        soff2.resize((size_t)nr + 1);
+        strm2.reserve(nops + (uint64_t)nzero);
+        for (int64_t r = 0; r < nr; r++) {
+            soff2[(size_t)r] = strm2.size();
+            const uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
+            if (o1 == o0) strm2.push_back(0u);
+            else strm2.insert(strm2.end(), p->cigar + o0, p->cigar + o1);
+        }
+        soff2[(size_t)nr] = strm2.size();
+        soff = soff2.data();
+        strm = strm2.data();
     }
-    poff[(size_t)nr] = pw;
-    bkt_off[(size_t)nt] = (int64_t)bkt.size();
+    const uint64_t nstream = nr > 0 ? soff[nr] : 0;
+    // ---- ranges of the index build: ~T stream ops each, cut at read starts and contig starts
+    const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / 65536, 2048), 1ull << 26);
+    std::vector<std::vector<uint64_t>> pt((size_t)nt);
+    parallel_for((size_t)nt, 16, [&](size_t t) {
+        for (int64_t r = p->tid_off[t], r1 = p->tid_off[t + 1]; r < r1;) {
+            pt[t].push_back((uint64_t)r);
+            const uint64_t s0 = soff[r];
+            for (r++; r < r1 && soff[r] - s0 < T; r++) {}
+        }
+    });
+    std::vector<uint64_t> part;
+    for (int32_t t = 0; t < nt; t++) part.insert(part.end(), pt[(size_t)t].begin(), pt[(size_t)t].end());
+    part.push_back((uint64_t)nr);
+    if (part.size() - 1 > 0xffffffffull) return fail(c, SVT_EINVAL, "pileup: %s", "too many index ranges");
+    c->n_ranges = (uint32_t)(part.size() - 1);
     c->load_stats.host_ms = ms_since(t_start);
+
     const clk::time_point t_up = clk::now();
     svt_status s;
     if ((s = upload(c, c->d_pos, p->pos, (size_t)nr))) return s;
     if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
     if ((s = upload(c, c->d_rec, rec.data(), (size_t)nr))) return s;
-    if ((s = upload(c, c->d_off64, poff.data(), poff.size()))) return s;
+    if ((s = upload(c, c->d_off64, soff, nr > 0 ? (size_t)nr + 1 : 0, nr > 0 ? 0 : 1))) return s;
     if ((s = upload(c, c->d_bkt, bkt.data(), bkt.size()))) return s;
     if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
     if (nt > 0) { if ((s = upload(c, c->d_tid_off, p->tid_off, (size_t)nt + 1))) return s; }
     else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
-    // padded arena: read r's ops at poff[r], zero words (0M) up to the next multiple of
-    // ALIGN_OPS, then CIGAR_PAD zero words; filled on the device from the caller's unpadded
-    // words together with the chunk index (one word per CHUNK arena words)
-    if ((s = upload<uint32_t>(c, c->d_cigar, nullptr, 0, (size_t)pw + CIGAR_PAD))) return s;
-    if ((s = upload<uint32_t>(c, c->d_chunk, nullptr, 0, (size_t)(pw / CHUNK) + CHUNK_PAD))) return s;
-    if ((s = upload<uint4>(c, c->d_rec2, nullptr, 0, (size_t)std::max<int64_t>(nr, 1)))) return s;
-    if (nr > 0) {
-        // pass 1 (pack_kernel): padded arena, chunk index, walk ends, per-read counts; device
-        // exclusive scans of the counts; pass 2: the gather variant's lists (event_kernel for
-        // the event walk, span_kernel for the span walk).  Only the scan totals come back.
-        const size_t S = (size_t)nr + 1;   // count-array stride: n_reads counts + a zero
-        uint32_t *d_raw = nullptr;
-        uint64_t *d_raw_off = nullptr, *d_cnt = nullptr;
-        void *d_tmp = nullptr;
-        size_t tmp_bytes = 0;
-        hipError_t e = hipMalloc(&d_raw, std::max<uint64_t>(nops, 1) * 4);
-        if (e == hipSuccess) e = hipMalloc(&d_raw_off, S * 8);
-        if (e == hipSuccess) e = hipMalloc(&d_cnt, 5 * S * 8);
-        if (e == hipSuccess) e = hipMemset(d_cnt, 0, 5 * S * 8);
-        if (e == hipSuccess && nops) e = hipMemcpy(d_raw, p->cigar, nops * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d_raw_off, p->cig_off, S * 8, hipMemcpyHostToDevice);
-        c->load_stats.upload_ms = ms_since(t_up);
-        hipEvent_t ev[2] = {nullptr, nullptr};
-        for (int k = 0; k < 2 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
-        if (e == hipSuccess) e = hipEventRecord(ev[0], nullptr);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, d_raw, d_raw_off,
-                               c->d_off64, c->d_rec, c->d_cigar, c->d_chunk, c->d_rec2, d_cnt, (int64_t)S, (int64_t)nr);
-            e = hipGetLastError();
-        }
-        // out[0 .. S) = exclusive prefix sums of cnt[k*S .. k*S + S); returns out[S-1] (the total)
-        auto scan = [&](int k, uint64_t *&out, uint64_t &total) {
-            if (e != hipSuccess) return;
-            e = hipMalloc(&out, S * 8);
-            if (e != hipSuccess) return;
-            c->dev_bytes += S * 8;
-            size_t need = 0;
-            e = hipcub::DeviceScan::ExclusiveSum(nullptr, need, d_cnt + (size_t)k * S, out, (int)S, nullptr);
-            if (e == hipSuccess && need > tmp_bytes) {
-                hfree(d_tmp);
-                e = hipMalloc(&d_tmp, need);
-                tmp_bytes = e == hipSuccess ? need : 0;
-            }
-            if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_cnt + (size_t)k * S, out, (int)S,
-                                                                     nullptr);
-            if (e == hipSuccess) e = hipMemcpy(&total, out + (S - 1), 8, hipMemcpyDeviceToHost);
-        };
-        if (S > 0x7fffffffull) e = hipErrorInvalidValue;   // hipcub item count is an int
-        // each read's first I >= 50 op in the pileup-wide (read, op) order of the allele-consensus
-        // sequences (svt_load_insseq), and the slow-read prefix counts
-        uint64_t n_slow = 0, n_ev = 0, nD = 0, nI = 0;
-        scan(1, c->d_insbase, c->n_ins);
-        scan(4, c->d_slowpre, n_slow);
-        hfree(d_raw);
-        hfree(d_raw_off);
-        if (c->gather == G_EVENT) {
-            scan(0, c->d_evoff, n_ev);
-            if (e == hipSuccess) e = hipMalloc(&c->d_ev, std::max<uint64_t>(n_ev, 1) * sizeof(uint2));
-            if (e == hipSuccess) {
-                c->dev_bytes += std::max<uint64_t>(n_ev, 1) * sizeof(uint2);
-                hipLaunchKernelGGL(event_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
-                                   c->d_off64, c->d_rec, c->d_rec2, c->d_evoff, c->d_ev, (int64_t)nr);
-                e = hipGetLastError();
-            }
-        }
-        if (c->gather == G_SPAN) {
-            scan(2, c->d_spoffD, nD);
-            scan(3, c->d_spoffI, nI);
-            if (e == hipSuccess) e = hipMalloc(&c->d_spD, std::max<uint64_t>(nD, 1) * sizeof(uint4));
-            if (e == hipSuccess) e = hipMalloc(&c->d_spI, std::max<uint64_t>(nI, 1) * sizeof(uint4));
-            if (e == hipSuccess) {
-                c->dev_bytes += (std::max<uint64_t>(nD, 1) + std::max<uint64_t>(nI, 1)) * sizeof(uint4);
-                hipLaunchKernelGGL(span_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, nullptr, c->d_cigar,
-                                   c->d_off64, c->d_rec, c->d_rec2, c->d_spoffD, c->d_spoffI, c->d_spD, c->d_spI,
-                                   (int64_t)nr);
-                e = hipGetLastError();
-            }
-        }
-        if (e == hipSuccess) e = hipEventRecord(ev[1], nullptr);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        if (e == hipSuccess) {
-            float a = 0.f;
-            e = hipEventElapsedTime(&a, ev[0], ev[1]);
-            c->load_stats.index_ms = (double)a;
-        }
-        for (int k = 0; k < 2; k++)
-            if (ev[k]) (void)hipEventDestroy(ev[k]);
-        hfree(d_cnt);
-        hfree(d_tmp);
-        hfree(d_raw);
-        hfree(d_raw_off);
-        if (e != hipSuccess) return fail(c, SVT_EDEVICE, "pileup index: %s", hipGetErrorString(e));
-    } else {
-        if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, 1))) return s;
-        if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, 1))) return s;
-    }
-    // variant arrays the pileup did not need: one zero element each (kernels never read them)
-    if (!c->d_ev && (s = upload<uint2>(c, c->d_ev, nullptr, 0, 1))) return s;
-    if (!c->d_evoff && (s = upload<uint64_t>(c, c->d_evoff, nullptr, 0, 1))) return s;
-    if (!c->d_spD && (s = upload<uint4>(c, c->d_spD, nullptr, 0, 1))) return s;
-    if (!c->d_spI && (s = upload<uint4>(c, c->d_spI, nullptr, 0, 1))) return s;
-    if (!c->d_spoffD && (s = upload<uint64_t>(c, c->d_spoffD, nullptr, 0, 1))) return s;
-    if (!c->d_spoffI && (s = upload<uint64_t>(c, c->d_spoffI, nullptr, 0, 1))) return s;
+    if ((s = upload(c, c->d_cigar, strm, (size_t)nstream, STREAM_PAD))) return s;
+    if ((s = upload(c, c->d_part, part.data(), part.size()))) return s;
+    const size_t S = (size_t)nr + 1;
+    if ((s = upload<uint2>(c, c->d_rec2, nullptr, 0, std::max<size_t>((size_t)nr, 1)))) return s;
+    if ((s = upload<uint64_t>(c, c->d_spoffD, nullptr, 0, S))) return s;
+    if ((s = upload<uint64_t>(c, c->d_spoffI, nullptr, 0, S))) return s;
+    if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, S))) return s;
+    if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, S))) return s;
+    if ((s = upload<uint32_t>(c, c->d_wtot, nullptr, 0, std::max<size_t>((size_t)c->n_ranges, 1) * IX_NTOT))) return s;
+    if ((s = upload<uint64_t>(c, c->d_wbase, nullptr, 0, std::max<size_t>((size_t)c->n_ranges, 1) * IX_NTOT))) return s;
+    if ((s = upload<uint64_t>(c, c->d_tot, nullptr, 0, IX_NTOT))) return s;
+    c->load_stats.upload_ms = ms_since(t_up);
     c->n_targets = nt;
     c->n_reads = nr;
     c->n_ops = nops;
+    if (nr > 0) {
+        double ims = 0;
+        if ((s = build_index(c, nullptr, true, &ims))) return s;
+        c->load_stats.index_ms = ims;
+        const uint64_t R = (uint64_t)nr;
+        c->load_stats.span_events = c->n_evD + c->n_evI;
+        c->load_stats.lead_blocks = c->n_lead_blocks;
+        c->load_stats.slow_reads = c->n_slow;
+        c->load_stats.index_bytes = 8ull * nstream + 2ull * (24ull + 12ull) * R + 32ull * R +
+                                    16ull * (c->n_evD + c->n_evI) + 144ull * c->n_lead_blocks;
+    } else {
+        for (auto *pp : {&c->d_spD, &c->d_spI})
+            if ((s = upload<uint4>(c, *pp, nullptr, 0, 1))) return s;
+        for (auto *pp : {&c->d_lcig, &c->d_lchunk})
+            if ((s = upload<uint32_t>(c, *pp, nullptr, 0, LEAD_PAD))) return s;
+    }
+    HIP_TRY(c, hipDeviceSynchronize());
     c->loaded = true;
-    if (nr == 0) c->load_stats.upload_ms = ms_since(t_up);
     c->load_stats.total_ms = ms_since(t_start);
     return SVT_OK;
 }
@@ -3458,6 +2673,17 @@ svt_status svt_load_pileup(svt_ctx *c, const svt_pileup_view *p) {
     // every device gets the whole pileup (n = device count: one "item" per device)
     const size_t D = 1 + c->subs.size();
     return for_devices(c, D, [&](svt_ctx *x, size_t lo, size_t hi) { return lo < hi ? load_1(x, p) : SVT_OK; });
+}
+
+svt_status svt_reindex(svt_ctx *c, void *stream) {
+    if (!c) return SVT_EINVAL;
+    if (!c->loaded) return fail(c, SVT_ESTATE, "%s", "svt_load_pileup not called");
+    DEV_GUARD(c);
+    if (c->n_reads == 0) return SVT_OK;
+    const hipStream_t st = (hipStream_t)stream;
+    svt_status s = order_on(c, st);   // after every launch already issued (they read the index)
+    if (s) return s;
+    return build_index(c, st, false, nullptr);
 }
 
 svt_status svt_last_load_stats(const svt_ctx *c, svt_load_stats *out) {
@@ -3530,21 +2756,12 @@ static svt_status run_batch_1(svt_ctx *c, const svt_locus *loci, size_t n, svt_r
         w->range_reads = k[W_RANGE]; w->list_reads = k[W_LREADS]; w->list_entries = k[W_LENTRIES];
         w->stop_searches = k[W_STOPS]; w->stop_chunk_words = k[W_STOPCH];
         w->span_bounds = k[W_SQUERIES]; w->span_events = k[W_SPAN];
-        // algorithmic bytes (DESIGN.md "Roofline"): locus in + result out, two bucket words per
-        // search pair, the search entries, per stop search the chunk words scanned, the word
-        // before the break chunk and its 8 CIGAR words; then per variant --
-        //   span:  the two span bounds of a query and its 16-B events;
-        //   event: rec + rec2 of every yielded read and rec of every overlap-failing one in
-        //          range, list offsets and list entries past the inline one
-        const uint64_t common = 24ull * n + 32ull * w->queries + 4ull * w->probe_entries +
-                                36ull * w->stop_searches + 4ull * w->stop_chunk_words;
-        if (c->gather == G_SPAN)
-            w->event_bytes = common + 16ull * w->span_bounds + 16ull * w->span_events;
-        else if (c->gather == G_EVENT)
-            w->event_bytes = common + 32ull * w->reads + 16ull * (w->range_reads - std::min(w->range_reads, w->reads)) +
-                             8ull * w->list_reads + 8ull * w->list_entries;
-        else
-            w->event_bytes = 24ull * n + 12ull * w->reads + 4ull * w->ops_walked;   // the variants walk CIGARs
+        // algorithmic bytes of the span walk (DESIGN.md "Roofline"): locus in + result out, two
+        // bucket words per search pair, the search entries, the two span bounds of a query and
+        // its 16-B events, per stop search the chunk words scanned, the word before the break
+        // chunk and its 8 CIGAR words
+        w->event_bytes = 24ull * n + 32ull * w->queries + 4ull * w->probe_entries + 36ull * w->stop_searches +
+                         4ull * w->stop_chunk_words + 16ull * w->span_bounds + 16ull * w->span_events;
     }
     return SVT_OK;
 }
@@ -3651,11 +2868,7 @@ static svt_status sw_1(svt_ctx *c, const svt_sw_query *q, size_t n, int32_t wind
             a.sw_sub = d_sub;
             a.sw_out = d_res;
             const dim3 grid((unsigned)((ns + WPB - 1) / WPB)), block(64 * WPB);
-            if (c->gather == G_SPAN) hipLaunchKernelGGL(sw_kernel<G_SPAN>, grid, block, 0, nullptr, a);
-            else if (c->gather == G_EVENT) hipLaunchKernelGGL(sw_kernel<G_EVENT>, grid, block, 0, nullptr, a);
-            else if (c->gather == G_INDEX) hipLaunchKernelGGL(sw_kernel<G_INDEX>, grid, block, 0, nullptr, a);
-            else if (c->gather == G_STREAM) hipLaunchKernelGGL(sw_kernel<G_STREAM>, grid, block, 0, nullptr, a);
-            else hipLaunchKernelGGL(sw_kernel<G_PERREAD>, grid, block, 0, nullptr, a);
+            hipLaunchKernelGGL(sw_kernel<G_SPAN>, grid, block, 0, nullptr, a);
             chk(hipGetLastError(), "sw_kernel: %s");
         }
         if (s == SVT_OK) {

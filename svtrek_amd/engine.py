@@ -103,6 +103,11 @@ class Engine:
         self._check(self.lib.svt_refine_device_records(self._h, C.c_void_p(d_loci), n, C.c_void_p(d_index or 0),
                                                        int(index_base), C.c_void_p(d_rec), C.c_void_p(stream or 0)))
 
+    def reindex(self, stream: int | None = None) -> None:
+        """Rebuild the device index of the loaded pileup on a hipStream_t handle (svt_reindex:
+        asynchronous, no host work, results unchanged)."""
+        self._check(self.lib.svt_reindex(self._h, C.c_void_p(stream or 0)))
+
     def sync(self, stream: int | None = None) -> None:
         self._check(self.lib.svt_sync(self._h, C.c_void_p(stream or 0)))
 
@@ -179,12 +184,14 @@ class Engine:
         """Timings (ms) of the last load_pileup: host pass, H2D copies, device index build."""
         st = SvtLoadStats()
         self._check(self.lib.svt_last_load_stats(self._h, C.byref(st)))
-        return {k: round(getattr(st, k), 3) for k, _ in SvtLoadStats._fields_}
+        return {k: (round(v, 3) if isinstance(v, float) else int(v))
+                for k, v in ((k, getattr(st, k)) for k, _ in SvtLoadStats._fields_)}
 
     def close(self) -> None:
         if getattr(self, "_h", None):
             self.lib.svt_close(self._h)
             self._h = None
+        self._pileup = None   # the host arrays (a large pileup's memory) are no longer pinned here
 
     def __del__(self):
         try:

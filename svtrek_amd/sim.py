@@ -36,6 +36,7 @@ class _SimConfig(C.Structure):
         ("p_noise_sv", C.c_double),
         ("p_clip_ends", C.c_double),
         ("p_exotic", C.c_double),
+        ("par_contigs", C.c_int32),
     ]
 
 
@@ -61,6 +62,7 @@ class SimConfig:
     p_noise_sv: float = 0.05
     p_clip_ends: float = 0.10
     p_exotic: float = 0.0
+    par_contigs: int = 0
 
     def to_c(self) -> _SimConfig:
         return _SimConfig(**{f.name: getattr(self, f.name) for f in fields(self)})
@@ -80,7 +82,7 @@ WORKLOADS = {
                                          rho=1 / 500, spacing=3100, sv_max_len=1000, first_offset=25000),
     "cfg5_100k_60x_ul_ont": SimConfig(seed=505, n_targets=8, n_loci=100000, del_frac=0.5, coverage=60.0,
                                       read_len_mean=50000, read_len_sd=10000, read_len_min=5000, rho=1 / 25,
-                                      spacing=40000),
+                                      spacing=40000, par_contigs=2),
 }
 
 
@@ -115,11 +117,14 @@ def generate(cfg: SimConfig, keep_handle: bool = False) -> SimResult:
     nl = lib.sim_n_loci(h)
 
     def arr(fn, dtype, n):
+        """The C array as numpy: a zero-copy view when the handle is kept (the Pileup keeps it
+        alive; cfg5's 9.6 G CIGAR words are never copied), else a copy."""
         p = getattr(lib, fn)(h)
         if n == 0:
             return np.zeros(0, dtype=dtype)
         buf = (C.c_char * (n * np.dtype(dtype).itemsize)).from_address(p)
-        return np.frombuffer(buf, dtype=dtype, count=n).copy()
+        a = np.frombuffer(buf, dtype=dtype, count=n)
+        return a if keep_handle else a.copy()
 
     pile = Pileup(
         tid_off=arr("sim_tid_off", np.int64, nt + 1),
@@ -136,7 +141,9 @@ def generate(cfg: SimConfig, keep_handle: bool = False) -> SimResult:
     loci["chrom"] = raw[:, 1]
     loci["pos"] = raw[:, 2].astype(np.uint32)
     loci["end"] = raw[:, 3].astype(np.uint32)
-    truth = arr("sim_truth", np.int32, nl * 2).reshape(-1, 2)
+    truth = arr("sim_truth", np.int32, nl * 2).reshape(-1, 2).copy()
+    if keep_handle:
+        pile._keepalive.append(hd)
     return SimResult(pile, loci, truth, hd if keep_handle else None)
 
 

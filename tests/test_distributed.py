@@ -166,7 +166,7 @@ def test_gloo_bench_shard_and_gather_path(tmp_path, world):
     np.testing.assert_array_equal(got.view(np.uint32), O.refine_batch(r.pileup, r.loci).view(np.uint32))
 
 
-def _audt_worker(rank, world, port, bam, outdir, fail_rank):
+def _audt_worker(rank, world, port, bam, outdir, fail_rank, fail_kind="refine"):
     """audt_dist.run_rank on gloo: BAI region read + halo trim per rank, status all-reduce,
     gather; the oracle stands in for the GPU engine (test infrastructure)."""
     import torch.distributed as dist
@@ -181,13 +181,18 @@ def _audt_worker(rank, world, port, bam, outdir, fail_rank):
     seen = {}
 
     def refine(pl, mine):
-        if rank == fail_rank:
+        if rank == fail_rank and fail_kind == "refine":
             raise ValueError("injected failure")
         seen["reads"] = pl.n_reads
         return O.refine_batch(pl, mine)
 
+    def parse():   # a failure before the shard (VCF parse) must not hang the others
+        if rank == fail_rank and fail_kind == "parse":
+            raise ValueError("injected failure")
+        return loci
+
     try:
-        res = audt_dist.run_rank(bam, loci, Params(), 2, refine, world, rank)
+        res = audt_dist.run_rank(bam, parse, Params(), 2, refine, world, rank)
         if rank == 0:
             np.save(os.path.join(outdir, "res.npy"), res.view(np.uint32).reshape(-1, 2))
         np.save(os.path.join(outdir, f"reads{rank}.npy"), np.array([seen.get("reads", 0)]))
@@ -198,8 +203,8 @@ def _audt_worker(rank, world, port, bam, outdir, fail_rank):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,fail_rank", [(2, -1), (3, -1), (2, 1)])
-def test_gloo_audt_dist_region_shards(tmp_path, world, fail_rank):
+@pytest.mark.parametrize("world,fail_rank,fail_kind", [(2, -1, ""), (3, -1, ""), (2, 1, "refine"), (3, 0, "parse")])
+def test_gloo_audt_dist_region_shards(tmp_path, world, fail_rank, fail_kind):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
@@ -209,7 +214,8 @@ def test_gloo_audt_dist_region_shards(tmp_path, world, fail_rank):
     bam = str(tmp_path / "c.bam")
     sim.write_bam(r, bam, with_seq=True, level=1)
     sim.write_vcf(r.loci, str(tmp_path / "c.vcf"))
-    mp.spawn(_audt_worker, args=(world, _free_port(), bam, str(tmp_path), fail_rank), nprocs=world, join=True)
+    mp.spawn(_audt_worker, args=(world, _free_port(), bam, str(tmp_path), fail_rank, fail_kind), nprocs=world,
+             join=True)
     if fail_rank >= 0:   # every rank stops with an error, none hangs in the gather
         for k in range(world):
             assert (tmp_path / f"err{k}.txt").exists()

@@ -119,26 +119,43 @@ def test_span_walk_counters(engine_factory):
     _same(eng.refine(r.loci), O.refine_batch(r.pileup, r.loci, threads=8))
 
 
-def test_event_walk_counters(engine_factory):
-    """svt_work's event-walk counters: internally consistent and event_bytes = their sum at
-    the documented sizes; the counting launch's results equal the plain launch's."""
-    r = _workload(n_loci=4000, seed=64)
-    eng = engine_factory(gather="event")
+def test_lane_count_lane_redo_counters(engine_factory):
+    """a lane launch, a counting launch, then a smaller lane launch -- the
+    third must start its left-over list from zero (two counters alternating on lane launches
+    only), so no stale window of the first batch is re-run out of bounds.  Forced lane kernel
+    (SVTREK_LANE_W) at both sizes; every result checked against the oracle."""
+    r = _workload(n_loci=6000, seed=66)
+    prm = Params(consensus_min_count=1)   # more windows with big bands -> left-overs in every launch
+    eng = engine_factory(prm, gather="span")   # lane kernel<32> at every batch size
     eng.load_pileup(r.pileup)
-    w = eng.count_work(r.loci)
-    n = len(r.loci)
-    assert w["queries"] <= w["windows"] and w["queries"] > 0.9 * w["windows"]
-    assert w["range_reads"] >= w["reads"] > 0
-    assert w["probe_entries"] >= 2 * w["queries"] * 0.5
-    assert w["list_entries"] >= w["list_reads"]
-    assert w["stop_chunk_words"] >= w["stop_searches"]
-    exp = (24 * n + 32 * w["queries"] + 4 * w["probe_entries"] + 32 * w["reads"]
-           + 16 * (w["range_reads"] - w["reads"]) + 8 * w["list_reads"] + 8 * w["list_entries"]
-           + 36 * w["stop_searches"] + 4 * w["stop_chunk_words"])
-    assert w["event_bytes"] == exp
-    # the event walk reads far fewer bytes than the reference's CIGAR walk touches
-    assert w["event_bytes"] < 24 * n + 12 * w["reads"] + 4 * w["ops_walked"]
-    _same(eng.refine(r.loci), O.refine_batch(r.pileup, r.loci, threads=8))
+    big, small = r.loci, r.loci[: len(r.loci) // 5]
+    want_big = O.refine_batch(r.pileup, big, prm, threads=8)
+    want_small = O.refine_batch(r.pileup, small, prm, threads=8)
+    for _ in range(2):
+        _same(eng.refine(big), want_big)
+        eng.count_work(big)
+        _same(eng.refine(small), want_small)
+        eng.count_work(small)
+        eng.count_work(big)
+        _same(eng.refine(small), want_small)
+
+
+def test_reindex_keeps_results(engine_factory):
+    """svt_reindex rebuilds the device index in place (bench.py's step): results before and
+    after, and after several rebuilds interleaved with refines, equal the oracle's."""
+    import torch
+    r = _workload(n_loci=3000, seed=67)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    want = O.refine_batch(r.pileup, r.loci, threads=8)
+    _same(eng.refine(r.loci), want)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        eng.reindex(s)
+    eng.sync(s)
+    _same(eng.refine(r.loci), want)
+    eng.reindex()
+    _same(eng.refine(r.loci), want)
 
 
 def test_locus_dtype_layout():

@@ -67,3 +67,38 @@ def test_cfg4_full_parity(engine_factory):
         (ow["windows"], ow["reads"], ow["ops_walked"], ow["candidates"])
     assert w["spilled_windows"] > 0          # the spill path ran at scale, and agreed
     assert len(got) == 1_000_000
+
+
+@pytest.mark.timeout(900)
+def test_cfg5_full_parity(engine_factory):
+    """BASELINE config 5 at full size: 100k DEL+INS loci over 8 contigs of 60x ultra-long
+    (50 kb, ~2000 ops/read) reads -- 9 G CIGAR ops (36 GB), generated zero-copy and walked by
+    the device index build; every locus, the work counters and the spilled windows vs the
+    oracle (16 threads)."""
+    import sys
+    import time
+    cfg = sim.WORKLOADS["cfg5_100k_60x_ul_ont"]
+    t0 = time.time()
+    r = sim.generate(cfg, keep_handle=True)
+    print(f"cfg5: {r.pileup.n_reads} reads, {r.pileup.n_ops} ops, generated in {time.time() - t0:.1f} s",
+          file=sys.stderr, flush=True)
+    eng = engine_factory()
+    try:
+        eng.load_pileup(r.pileup)
+        st = eng.load_stats()
+        print(f"cfg5: load {st}", file=sys.stderr, flush=True)
+        assert st["slow_reads"] == 0 and st["lead_blocks"] > 0
+        got = eng.refine(r.loci)
+        want, ow = O.refine_batch(r.pileup, r.loci, threads=16, with_work=True)
+        bad = np.nonzero((got["start"] != want["start"]) | (got["end"] != want["end"]))[0]
+        assert len(bad) == 0, f"{len(bad)} loci differ, first {r.loci[bad[0]]}: gpu {got[bad[0]]} oracle {want[bad[0]]}"
+        w = eng.count_work(r.loci)
+        assert (w["windows"], w["reads"], w["ops_walked"], w["candidates"]) == \
+            (ow["windows"], ow["reads"], ow["ops_walked"], ow["candidates"])
+        print(f"cfg5: work {w}", file=sys.stderr, flush=True)
+        eng.reindex()
+        got2 = eng.refine(r.loci)
+        assert (got2 == got).all()
+        assert len(got) == 100_000
+    finally:
+        eng.close()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Run ON THE GPU BOX: GPU parity tests, then bench (stream + perread gather variants).
+# Run ON THE GPU BOX: smoke, GPU parity tests, then bench.
 # Stops at the first step that crashes / times out; a plain test failure (rc 1) still
 # lets the benches run so one call yields both signals.
 set -u
@@ -21,6 +21,4 @@ tail -5 "$OUT/pytest.log"
 if [ $rc -gt 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
 run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
 tail -1 "$OUT/bench.log"
-SVTREK_GATHER=index run bench_streamvar 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit $?
-tail -1 "$OUT/bench_streamvar.log"
 exit $rc

@@ -1,14 +1,15 @@
 """Turn a tools/gpu_profile.sh run into the committed profile + profiles/traffic.json.
 
-    python tools/make_traffic.py gpurun_out/prof_TAG profiles/TAG [--workload W] [--kernel K]
+    python tools/make_traffic.py gpurun_out/prof_TAG profiles/TAG [--workload W]
 
 Copies the kernel stats / PMC CSVs and bench logs into profiles/TAG and writes
-profiles/traffic.json for the timed kernel (default refine_span_kernel): HBM bytes per launch =
+profiles/traffic.json entries for every kernel of bench.py's step and for the step itself
+(their sum): HBM bytes per launch =
 read bytes from the L2 fabric read requests by size class (TCC_EA0_RDREQ_{32B,64B,128B}:
 32/64/128 B each; cross-checked against 2 x FETCH_SIZE, which gfx950 tallies at 64 B per
 128-B request, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, median over the profiled
-launches.  bench.py reports it as roofline.traffic when engine version, workload and kernel
-match.
+launches.  bench.py reports the step entry as roofline.traffic when engine version and
+workload match.
 """
 from __future__ import annotations
 
@@ -32,45 +33,32 @@ def med(v: list[float]) -> float | None:
     return statistics.median(v) if v else None
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("src")
-    ap.add_argument("dst")
-    ap.add_argument("--workload", default="cfg4_1m_delins_30x_hifi")
-    ap.add_argument("--kernel", default="refine_span_kernel")
-    a = ap.parse_args()
-    os.makedirs(a.dst, exist_ok=True)
-    copies = {"trace/run_kernel_stats.csv": "kernel_stats.csv", "pmc_fetch/run_counter_collection.csv":
-              "pmc_fetch_size.csv", "pmc_write/run_counter_collection.csv": "pmc_write_size.csv",
-              "pmc_rdreq/run_counter_collection.csv": "pmc_rdreq.csv",
-              "pmc_dram/run_counter_collection.csv": "pmc_dram.csv", "pmc_sq/run_counter_collection.csv": "pmc_sq.csv",
-              "trace.log": "bench_under_rocprof.log"}
-    for s, d in copies.items():
-        if os.path.exists(os.path.join(a.src, s)):
-            shutil.copy(os.path.join(a.src, s), os.path.join(a.dst, d))
-    j = lambda sub: os.path.join(a.src, sub, "run_counter_collection.csv")  # noqa: E731
-    fetch = med(counter_values(j("pmc_fetch"), a.kernel, "FETCH_SIZE"))
-    write = med(counter_values(j("pmc_write"), a.kernel, "WRITE_SIZE"))
-    n32 = med(counter_values(j("pmc_rdreq"), a.kernel, "TCC_EA0_RDREQ_32B_sum"))
-    n64 = med(counter_values(j("pmc_rdreq"), a.kernel, "TCC_EA0_RDREQ_64B_sum"))
-    n128 = med(counter_values(j("pmc_rdreq"), a.kernel, "TCC_EA0_RDREQ_128B_sum"))
-    dram32 = med(counter_values(j("pmc_dram"), a.kernel, "TCC_EA0_RDREQ_DRAM_32B_sum"))
-    ver = None
-    with open(os.path.join(a.src, "trace.log")) as f:
-        for line in f:
-            if line.startswith("{"):
-                ver = json.loads(line).get("engine_version", ver)
+STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's kernel name)
+    "index_kernel<census>": "index_kernel<false>",
+    "range_scan_kernel": "range_scan_kernel",
+    "index_kernel<emit>": "index_kernel<true>",
+    "refine_lane_kernel": "refine_lane_kernel",
+    "refine_redo_kernel": "refine_redo_kernel",
+}
+
+
+def kernel_bytes(src: str, kernel: str) -> dict | None:
+    j = lambda sub: os.path.join(src, sub, "run_counter_collection.csv")  # noqa: E731
+    fetch = med(counter_values(j("pmc_fetch"), kernel, "FETCH_SIZE"))
+    write = med(counter_values(j("pmc_write"), kernel, "WRITE_SIZE"))
+    n32 = med(counter_values(j("pmc_rdreq"), kernel, "TCC_EA0_RDREQ_32B_sum"))
+    n64 = med(counter_values(j("pmc_rdreq"), kernel, "TCC_EA0_RDREQ_64B_sum"))
+    n128 = med(counter_values(j("pmc_rdreq"), kernel, "TCC_EA0_RDREQ_128B_sum"))
+    dram32 = med(counter_values(j("pmc_dram"), kernel, "TCC_EA0_RDREQ_DRAM_32B_sum"))
+    if n128 is None and fetch is None:
+        return None
     if n128 is not None:
         rd = 32 * (n32 or 0) + 64 * (n64 or 0) + 128 * n128
         method_rd = "TCC_EA0_RDREQ_{32B,64B,128B}_sum x {32,64,128} B"
     else:
         rd = 2 * fetch * 1024
         method_rd = "2 x FETCH_SIZE"
-    out = {
-        "kernel": a.kernel,
-        "records": True,   # bench.py's launches write 16-B gather records
-        "workload": a.workload,
-        "engine_version": ver,
+    return {
         "read_bytes_per_launch": int(round(rd)),
         "write_bytes_per_launch": int(round((write or 0) * 1024)),
         "hbm_bytes_per_launch": int(round(rd + (write or 0) * 1024)),
@@ -81,8 +69,45 @@ def main() -> int:
         "method": f"rocprofv3 --pmc passes of tools/gpu_profile.sh, one counter group per pass; reads: {method_rd} "
                   "(2 x FETCH_SIZE agrees: gfx950 tallies a 128-B request at 64 B); writes: WRITE_SIZE; "
                   "median over the profiled launches",
-        "source": f"{a.dst}/pmc_*.csv",
     }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--workload", default="cfg4_1m_delins_30x_hifi")
+    a = ap.parse_args()
+    os.makedirs(a.dst, exist_ok=True)
+    copies = {"trace/run_kernel_stats.csv": "kernel_stats.csv", "pmc_fetch/run_counter_collection.csv":
+              "pmc_fetch_size.csv", "pmc_write/run_counter_collection.csv": "pmc_write_size.csv",
+              "pmc_rdreq/run_counter_collection.csv": "pmc_rdreq.csv",
+              "pmc_dram/run_counter_collection.csv": "pmc_dram.csv", "pmc_sq/run_counter_collection.csv": "pmc_sq.csv",
+              "trace.log": "bench_under_rocprof.log"}
+    for s_, d in copies.items():
+        if os.path.exists(os.path.join(a.src, s_)):
+            shutil.copy(os.path.join(a.src, s_), os.path.join(a.dst, d))
+    ver = None
+    with open(os.path.join(a.src, "trace.log")) as f:
+        for line in f:
+            if line.startswith("{"):
+                ver = json.loads(line).get("engine_version", ver)
+    new = []
+    step = {"read_bytes_per_launch": 0, "write_bytes_per_launch": 0, "hbm_bytes_per_launch": 0}
+    for label, sub in STEP.items():
+        kb = kernel_bytes(a.src, sub)
+        if kb is None:
+            continue
+        e = {"kernel": label, "records": True, "workload": a.workload, "engine_version": ver, **kb,
+             "source": f"{a.dst}/pmc_*.csv"}
+        new.append(e)
+        for k in step:
+            step[k] += kb[k]
+    if new:
+        new.append({"kernel": "step", "records": True, "workload": a.workload, "engine_version": ver, **step,
+                    "kernels": [e["kernel"] for e in new],
+                    "method": "sum over the step's kernels of each kernel's median bytes per launch (one launch "
+                              "of each per bench.py step)", "source": f"{a.dst}/pmc_*.csv"})
     # profiles/traffic.json: one entry per (engine version, workload, kernel, records)
     tpath = os.path.join(os.path.dirname(a.dst.rstrip("/")), "traffic.json")
     try:
@@ -92,10 +117,13 @@ def main() -> int:
     except (OSError, ValueError):
         old = []
     key = lambda e: (e.get("engine_version"), e.get("workload"), e.get("kernel"), bool(e.get("records")))  # noqa
-    entries = [e for e in old if key(e) != key(out)] + [out]
+    keys = {key(e) for e in new}
+    entries = [e for e in old if key(e) not in keys] + new
     with open(tpath, "w") as f:
         json.dump(entries, f, indent=1)
-    print(json.dumps(out))
+    for e in new:
+        print(json.dumps({k: e[k] for k in ("kernel", "read_bytes_per_launch", "write_bytes_per_launch",
+                                            "hbm_bytes_per_launch")}))
     return 0
 
 
