@@ -195,11 +195,15 @@ struct BaiLinear {
         if (!ok) err = "corrupt BAI: " + path;
         return ok;
     }
-    // Where a read of the records from (tid, beg) on starts; false = no such record.
+    // Where a read of the records from (tid, beg) on starts; false = no such record.  A zero
+    // entry is a window no record overlapped (older indexers leave those 0 instead of the next
+    // window's offset): virtual offset 0 is the BAM header, never a record, so the next
+    // non-zero entry -- of this contig or a later one -- is taken instead.
     bool start(int32_t tid, int64_t beg, uint64_t &voff) const {
         for (size_t t = (size_t)std::max(tid, 0); t < ioff.size(); t++) {
             const int64_t w = (int32_t)t == tid ? std::max<int64_t>(beg, 0) >> 14 : 0;
-            if (w < (int64_t)ioff[t].size()) { voff = ioff[t][(size_t)w]; return true; }
+            for (size_t k = (size_t)std::max<int64_t>(w, 0); k < ioff[t].size(); k++)
+                if (ioff[t][k] != 0) { voff = ioff[t][k]; return true; }
         }
         return false;
     }

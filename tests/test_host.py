@@ -188,6 +188,59 @@ def test_bam_region_read(tmp_path, region):
     assert info["records"] >= int(inside.sum())
 
 
+def _zero_empty_bai_windows(bai_path: str, pl) -> int:
+    """Rewrite a BAI the way older indexers leave it: linear-index windows no record overlaps
+    hold 0 (the sim writer fills them with the next window's offset).  Returns how many."""
+    import struct
+    data = open(bai_path, "rb").read()
+    o = 8
+    n_ref = struct.unpack_from("<i", data, 4)[0]
+    out = bytearray(data)
+    zeroed = 0
+    for t in range(n_ref):
+        n_bin = struct.unpack_from("<i", data, o)[0]
+        o += 4
+        for _ in range(n_bin):
+            n_chunk = struct.unpack_from("<i", data, o + 4)[0]
+            o += 8 + 16 * n_chunk
+        n_intv = struct.unpack_from("<i", data, o)[0]
+        o += 4
+        r0, r1 = int(pl.tid_off[t]), int(pl.tid_off[t + 1])
+        cov = np.zeros(n_intv, dtype=bool)
+        for p_, e_ in zip(pl.pos[r0:r1], pl.endpos[r0:r1]):
+            cov[int(p_) >> 14:((int(e_) - 1) >> 14) + 1] = True
+        for k in np.nonzero(~cov)[0]:
+            struct.pack_into("<Q", out, o + 8 * int(k), 0)
+            zeroed += 1
+        o += 8 * n_intv
+    open(bai_path, "wb").write(bytes(out))
+    return zeroed
+
+
+def test_bam_region_read_zero_linear_index(tmp_path):
+    """a BAI whose empty 16 kb windows hold 0 (older indexers) -- a region
+    starting in such a window seeks to the next non-zero entry, never to offset 0 (the
+    header), and still yields every record the region overlaps."""
+    cfg = sim.SimConfig(seed=33, n_targets=2, n_loci=20, del_frac=0.5, coverage=0.4, spacing=60000)
+    r = sim.generate(cfg, keep_handle=True)
+    path = str(tmp_path / "z.bam")
+    sim.write_bam(r, path, with_seq=False, level=1)
+    assert _zero_empty_bai_windows(path + ".bai", r.pileup) > 0
+    full, _ = host.read_bam(path, threads=2)
+    tids = np.repeat(np.arange(2), np.diff(full.tid_off))
+    for t0 in range(2):
+        r0, r1 = int(full.tid_off[t0]), int(full.tid_off[t0 + 1])
+        gaps = [int(full.endpos[r0:r1][:k + 1].max()) for k in range(r1 - r0 - 1)
+                if full.pos[r0 + k + 1] > full.endpos[r0:r0 + k + 1].max() + (1 << 15)]
+        for b0 in gaps[:3]:
+            b0 += 1 << 14   # a window no record overlaps
+            part, _ = host.read_bam(path, threads=2, region=(t0, b0, 1, 1 << 29))
+            pt = np.repeat(np.arange(2), np.diff(part.tid_off))
+            inside = (tids > t0) | ((tids == t0) & (full.endpos > b0))
+            key = lambda t, p, e: set(zip(t.tolist(), p.tolist(), e.tolist()))  # noqa: E731
+            assert key(tids[inside], full.pos[inside], full.endpos[inside]) <= key(pt, part.pos, part.endpos)
+
+
 @pytest.mark.parametrize("threads", [1, 3, 8])
 def test_vcf_batch_parse_and_format(threads):
     """svth_vcf_parse / svth_format_batch (multithreaded, '\\n'-aligned pieces) give the
