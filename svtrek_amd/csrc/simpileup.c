@@ -594,52 +594,137 @@ int sim_insseq(const sim_pileup *p, uint64_t seed, int32_t bp_jitter, int32_t er
 }
 
 /* ---------------------------------------------------------------- BAM writer */
+/* BGZF blocks are independent deflate streams, so the writer fills a batch of blocks and
+ * compresses them on several threads, then writes them in order.  Virtual offsets handed out
+ * while writing are (block index << 16 | in-block offset); the BAI is built afterwards with
+ * each block index mapped to its file offset. */
+#define BGZF_BLK 65280
+#define BGZF_BATCH 256
+#define BGZF_THREADS 16
 typedef struct {
     FILE *f;
-    uint8_t buf[65280];
-    size_t n;
+    uint8_t *ubuf;        /* BGZF_BATCH blocks of BGZF_BLK bytes */
+    uint8_t *cbuf;        /* BGZF_BATCH compressed blocks of <= 65536 bytes */
+    uint32_t *ulen, *clen;
+    size_t nb;            /* complete blocks in the batch */
+    size_t n;             /* bytes in the open block */
+    uint64_t blk;         /* blocks written before this batch */
+    uint64_t coff;        /* compressed bytes written so far */
+    uint64_t *boff;       /* file offset of every block written */
+    size_t capboff;
     int level;
     int err;
-    uint64_t coff;   /* compressed bytes written so far = the current block's file offset */
 } bgzf_w;
 
-/* BGZF virtual offset of the next byte written (SAM spec 4.1.1). */
-static uint64_t bgzf_voff(const bgzf_w *w) { return w->coff << 16 | (uint64_t)w->n; }
+/* virtual offset of the next byte written: (block index << 16 | in-block offset) */
+static uint64_t bgzf_voff(const bgzf_w *w) { return (w->blk + w->nb) << 16 | (uint64_t)w->n; }
 
-static void bgzf_flush(bgzf_w *w) {
-    if (w->err) return;
-    uint8_t out[65536];
+static int bgzf_block(uint8_t *out, const uint8_t *in, uint32_t n, int level, uint32_t *bsize) {
     z_stream zs;
     memset(&zs, 0, sizeof zs);
-    if (deflateInit2(&zs, w->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { w->err = 1; return; }
-    zs.next_in = w->buf; zs.avail_in = (uInt)w->n;
-    zs.next_out = out + 18; zs.avail_out = (uInt)(sizeof(out) - 26);
-    if (deflate(&zs, Z_FINISH) != Z_STREAM_END) { deflateEnd(&zs); w->err = 1; return; }
-    size_t clen = zs.total_out;
+    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return -1;
+    zs.next_in = (Bytef *)in; zs.avail_in = (uInt)n;
+    zs.next_out = out + 18; zs.avail_out = (uInt)(65536 - 26);
+    if (deflate(&zs, Z_FINISH) != Z_STREAM_END) { deflateEnd(&zs); return -1; }
+    size_t cl = zs.total_out;
     deflateEnd(&zs);
-    size_t bsize = clen + 26;   /* whole block */
+    size_t bs = cl + 26;   /* whole block */
     static const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
     memcpy(out, hdr, 16);
-    out[16] = (uint8_t)((bsize - 1) & 0xff);
-    out[17] = (uint8_t)((bsize - 1) >> 8);
-    uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), w->buf, (uInt)w->n);
-    uint8_t *t = out + 18 + clen;
+    out[16] = (uint8_t)((bs - 1) & 0xff);
+    out[17] = (uint8_t)((bs - 1) >> 8);
+    uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), in, (uInt)n);
+    uint8_t *t = out + 18 + cl;
     t[0] = crc & 0xff; t[1] = (crc >> 8) & 0xff; t[2] = (crc >> 16) & 0xff; t[3] = crc >> 24;
-    uint32_t isz = (uint32_t)w->n;
-    t[4] = isz & 0xff; t[5] = (isz >> 8) & 0xff; t[6] = (isz >> 16) & 0xff; t[7] = isz >> 24;
-    if (fwrite(out, 1, bsize, w->f) != bsize) w->err = 1;
-    w->coff += bsize;
-    w->n = 0;
+    t[4] = n & 0xff; t[5] = (n >> 8) & 0xff; t[6] = (n >> 16) & 0xff; t[7] = n >> 24;
+    *bsize = (uint32_t)bs;
+    return 0;
 }
+
+typedef struct { bgzf_w *w; size_t k0, nblk, step; int err; } bgzf_job;
+static void *bgzf_job_run(void *arg) {
+    bgzf_job *j = (bgzf_job *)arg;
+    for (size_t k = j->k0; k < j->nblk; k += j->step)
+        if (bgzf_block(j->w->cbuf + k * 65536, j->w->ubuf + k * BGZF_BLK, j->w->ulen[k], j->w->level, &j->w->clen[k]))
+            j->err = 1;
+    return NULL;
+}
+
+/* compress the batch's blocks (the open one too when `last`) and write them in order */
+static void bgzf_flush_batch(bgzf_w *w, int last) {
+    if (last && w->n) { w->ulen[w->nb++] = (uint32_t)w->n; w->n = 0; }
+    const size_t nb = w->nb;
+    if (w->err || nb == 0) { w->nb = 0; return; }
+    const size_t T = nb < BGZF_THREADS ? nb : BGZF_THREADS;
+    bgzf_job J[BGZF_THREADS];
+    pthread_t th[BGZF_THREADS];
+    int made[BGZF_THREADS] = {0};
+    for (size_t t = 0; t < T; t++) {
+        J[t] = (bgzf_job){w, t, nb, T, 0};
+        made[t] = pthread_create(&th[t], NULL, bgzf_job_run, &J[t]) == 0;
+        if (!made[t]) bgzf_job_run(&J[t]);
+    }
+    for (size_t t = 0; t < T; t++) {
+        if (made[t]) pthread_join(th[t], NULL);
+        if (J[t].err) w->err = 1;
+    }
+    if (w->blk + nb > w->capboff) {
+        size_t nc = w->capboff ? 2 * w->capboff : 1024;
+        while (nc < w->blk + nb) nc *= 2;
+        uint64_t *x = (uint64_t *)realloc(w->boff, nc * sizeof(uint64_t));
+        if (!x) { w->err = 1; return; }
+        w->boff = x; w->capboff = nc;
+    }
+    for (size_t k = 0; k < nb && !w->err; k++) {
+        w->boff[w->blk + k] = w->coff;
+        if (fwrite(w->cbuf + k * 65536, 1, w->clen[k], w->f) != w->clen[k]) w->err = 1;
+        w->coff += w->clen[k];
+    }
+    w->blk += nb;
+    w->nb = 0;
+}
+
 static void bgzf_put(bgzf_w *w, const void *data, size_t len) {
     const uint8_t *d = (const uint8_t *)data;
     while (len) {
-        size_t k = sizeof(w->buf) - w->n;
+        size_t k = BGZF_BLK - w->n;
         if (k > len) k = len;
-        memcpy(w->buf + w->n, d, k);
+        memcpy(w->ubuf + w->nb * BGZF_BLK + w->n, d, k);
         w->n += k; d += k; len -= k;
-        if (w->n == sizeof(w->buf)) bgzf_flush(w);
+        if (w->n == BGZF_BLK) {   /* block complete */
+            w->ulen[w->nb++] = BGZF_BLK;
+            w->n = 0;
+            if (w->nb == BGZF_BATCH) bgzf_flush_batch(w, 0);
+        }
     }
+}
+
+static bgzf_w *bgzf_open(const char *path, int level) {
+    bgzf_w *w = (bgzf_w *)calloc(1, sizeof(bgzf_w));
+    if (!w) return NULL;
+    w->ubuf = (uint8_t *)malloc((size_t)BGZF_BATCH * BGZF_BLK);
+    w->cbuf = (uint8_t *)malloc((size_t)BGZF_BATCH * 65536);
+    w->ulen = (uint32_t *)calloc(BGZF_BATCH, sizeof(uint32_t));
+    w->clen = (uint32_t *)calloc(BGZF_BATCH, sizeof(uint32_t));
+    w->f = fopen(path, "wb");
+    w->level = level < 0 ? 6 : level;
+    if (!w->ubuf || !w->cbuf || !w->ulen || !w->clen || !w->f) {
+        if (w->f) fclose(w->f);
+        free(w->ubuf); free(w->cbuf); free(w->ulen); free(w->clen); free(w);
+        return NULL;
+    }
+    return w;
+}
+
+/* file offset << 16 | in-block offset of a virtual offset handed out by bgzf_voff */
+static uint64_t bgzf_real(const bgzf_w *w, uint64_t v) {
+    const uint64_t b = v >> 16;
+    const uint64_t c = b < w->blk ? w->boff[b] : w->coff;   /* past the last block: EOF marker */
+    return c << 16 | (v & 0xffff);
+}
+
+static void bgzf_free(bgzf_w *w) {
+    free(w->ubuf); free(w->cbuf); free(w->ulen); free(w->clen); free(w->boff); free(w);
 }
 static void put32(bgzf_w *w, int32_t v) { uint8_t b[4] = {(uint8_t)v, (uint8_t)(v >> 8), (uint8_t)(v >> 16), (uint8_t)(v >> 24)}; bgzf_put(w, b, 4); }
 
@@ -749,16 +834,18 @@ int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level
 
 int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, int level, int32_t rtid, int64_t rbeg,
                          int64_t rend, int write_bai) {
-    bgzf_w *w = (bgzf_w *)calloc(1, sizeof(bgzf_w));
+    bgzf_w *w = bgzf_open(path, level);
     if (!w) return -1;
     bai_ref *bai = NULL;
     if (write_bai && !(bai = (bai_ref *)calloc((size_t)(p->n_targets > 0 ? p->n_targets : 1), sizeof(bai_ref)))) {
-        free(w);
+        fclose(w->f);
+        bgzf_free(w);
         return -1;
     }
-    w->f = fopen(path, "wb");
-    if (!w->f) { free(w); return -1; }
-    w->level = level < 0 ? 6 : level;
+    /* BAI entries, with virtual offsets mapped to file offsets once every block is written */
+    typedef struct { int32_t t; uint32_t bin; uint64_t vb, ve; int64_t pos, endpos; } pend_t;
+    pend_t *pend = NULL;
+    size_t npend = 0, cappend = 0;
     rng_t rng;
     rng_seed(&rng, 0x5eed5eedull);
     /* header */
@@ -812,7 +899,7 @@ int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, in
             if (need > rec_cap) {
                 rec_cap = need * 2;
                 uint8_t *x = (uint8_t *)realloc(rec, rec_cap);
-                if (!x) { free(rec); fclose(w->f); free(w); return -1; }
+                if (!x) { free(rec); free(pend); fclose(w->f); bgzf_free(w); bai_free(bai, p->n_targets); return -1; }
                 rec = x;
             }
             uint8_t *q = rec + 4;
@@ -848,17 +935,29 @@ int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, in
             memcpy(rec, &bs, 4);
             const uint64_t vbeg = bgzf_voff(w);
             bgzf_put(w, rec, (size_t)(q - rec));
-            if (bai && bai_add(&bai[t], (uint32_t)reg2bin(p->pos[r], p->endpos[r]), vbeg, bgzf_voff(w), p->pos[r],
-                               p->endpos[r])) w->err = 1;
+            if (bai) {
+                if (npend == cappend) {
+                    cappend = cappend ? 2 * cappend : 4096;
+                    pend_t *x = (pend_t *)realloc(pend, cappend * sizeof(pend_t));
+                    if (!x) { w->err = 1; break; }
+                    pend = x;
+                }
+                pend[npend++] = (pend_t){t, (uint32_t)reg2bin(p->pos[r], p->endpos[r]), vbeg, bgzf_voff(w), p->pos[r],
+                                         p->endpos[r]};
+            }
         }
     }
     free(rec);
-    if (w->n) bgzf_flush(w);
+    bgzf_flush_batch(w, 1);
     static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (!w->err && fwrite(eof, 1, 28, w->f) != 28) w->err = 1;
     int err = w->err;
     if (fclose(w->f)) err = 1;
-    free(w);
+    for (size_t k = 0; bai && !err && k < npend; k++)
+        if (bai_add(&bai[pend[k].t], pend[k].bin, bgzf_real(w, pend[k].vb), bgzf_real(w, pend[k].ve), pend[k].pos,
+                    pend[k].endpos)) err = 1;
+    free(pend);
+    bgzf_free(w);
     if (bai && !err) {
         size_t L = strlen(path);
         char *bp = (char *)malloc(L + 5);
