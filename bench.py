@@ -11,8 +11,9 @@ refines the g-th contiguous slice against only the reads its queries can reach
 ("scaling": "strong").
 
 A step is the whole per-locus path from the resident columnar pileup to refined calls:
-  1. the device index build (svt_reindex: index_kernel<census>, range_scan_kernel,
-     index_kernel<emit> -- every read's CIGAR walked once, refinement.c:118-159/:184-221/:295-318),
+  1. the device index build (svt_reindex: index_kernel<census> with a decoupled look-back scan
+     of its ranges, then index_kernel<emit> -- every read's CIGAR walked once,
+     refinement.c:118-159/:184-221/:295-318),
   2. one batched refine launch over the rank's slice (svt_refine_device_records:
      refine_lane_kernel + refine_redo_kernel; loci and 16-B result records resident in HBM),
   3. at N > 1, the one collective of the path: an RCCL gather to rank 0 of the slice's 16-B
@@ -124,8 +125,7 @@ def _engine_version() -> str:
     return version()
 
 
-STEP_KERNELS = ("index_kernel<census>", "range_scan_kernel", "index_kernel<emit>", "refine_lane_kernel",
-                "refine_redo_kernel")
+STEP_KERNELS = ("index_kernel<census>", "index_kernel<emit>", "refine_lane_kernel", "refine_redo_kernel")
 
 
 def _traffic(workload: str, kernel: str, records: bool) -> tuple[int | None, str | None]:
@@ -154,6 +154,9 @@ def main() -> int:
     ap.add_argument("--no-cold", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records check")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--emulate-shard", default=None, metavar="N:R",
+                    help="diagnostic, one process: run rank R's slice of an N-GPU run (its loci and halo reads) "
+                         "alone -- the per-rank work of the multi-GPU bench, measured on one GPU")
     ap.add_argument("--scale", type=float, default=1.0,
                     help="diagnostic: scale the workload's locus count (and so its genome) by this factor")
     args = ap.parse_args()
@@ -186,7 +189,11 @@ def main() -> int:
     gen_s = time.perf_counter() - t0
     params = Params()
     t0 = time.perf_counter()
-    rows, sl, spile = shard_workload(res.loci, res.pileup, params, world, rank)
+    if args.emulate_shard:
+        en, er = (int(x) for x in args.emulate_shard.split(":"))
+        rows, sl, spile = shard_workload(res.loci, res.pileup, params, en, er)
+    else:
+        rows, sl, spile = shard_workload(res.loci, res.pileup, params, world, rank)
     shard_s = time.perf_counter() - t0
     n_total, n = len(res.loci), len(sl)
     per = padded_rows(n_total, world)
@@ -261,7 +268,7 @@ def main() -> int:
     # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records)
     last = (args.steps - 1) % 2
     verified = None
-    if rank == 0 and (gather or world == 1) and not args.no_verify:
+    if rank == 0 and (gather or world == 1) and not args.no_verify and not args.emulate_shard:
         parts = pg.gathered(last)
         unpack_records(np.concatenate([p.cpu().numpy().view(np.uint32) for p in parts]), n_total)
         verified = True
@@ -289,7 +296,7 @@ def main() -> int:
         del flush
     eng.sync(sh)
 
-    total_loci = n_total * args.steps
+    total_loci = (n if args.emulate_shard else n_total) * args.steps
     value = total_loci / t_max
     ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
     achieved = ref_bytes / (step_ms * 1e-3) / 1e9
@@ -298,7 +305,7 @@ def main() -> int:
                                              (os.environ.get("SVTREK_LANE_W") or 2 * n >= 65536)) \
         else "refine_span_kernel"   # the engine's size-based pick (svt_engine.hip, launch)
     traffic, traffic_src = _traffic(args.workload, "step", records=True)
-    if args.scale != 1.0 or world > 1:
+    if args.scale != 1.0 or world > 1 or args.emulate_shard:
         traffic = traffic_src = None
     idx_bytes = int(load_stats.get("index_bytes", 0))
 
@@ -329,13 +336,14 @@ def main() -> int:
                        "parallelism": f"genomic row shard x{world}",
                        "gather": "16-B records, RCCL gather to rank 0, overlapped with the next launch"
                        if gather else None,
-                       **({"loci_scale": args.scale} if args.scale != 1.0 else {})},
+                       **({"loci_scale": args.scale} if args.scale != 1.0 else {}),
+                       **({"emulated_shard": args.emulate_shard} if args.emulate_shard else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_over_alg": round(traffic / ref_bytes, 4) if traffic else None,
                          "traffic_gbs": round(traffic / (step_ms * 1e-3) / 1e9, 2) if traffic else None,
                          "traffic_source": traffic_src,
-                         "kernel": "step = index build (" + ", ".join(STEP_KERNELS[:3]) + ") + refine (" +
+                         "kernel": "step = index build (" + ", ".join(STEP_KERNELS[:2]) + ") + refine (" +
                                    (refine_kernel + (", refine_redo_kernel" if refine_kernel == "refine_lane_kernel"
                                                      else "")) + ")",
                          "step_ms_mean": round(step_ms, 5),
@@ -349,8 +357,9 @@ def main() -> int:
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "CIGAR stream twice (4 B/op), 36 B/read per pass, 32 B/read offsets, "
-                                                "16 B/span event, 144 B/lead block (svt_load_stats.index_bytes)",
+                             "index_bytes_def": "CIGAR stream twice (4 B/op), 24 B/read read per pass + 4 B/read "
+                                                "rec word + 32 B/read offsets, 16 B/span event, 16 B/lead chunk unit "
+                                                "(svt_load_stats.index_bytes)",
                          },
                          "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
                                           "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),
@@ -359,7 +368,7 @@ def main() -> int:
                                                  "36 B/locus + 32 B/query + 4 B/search entry + 16 B/span bounds + "
                                                  "16 B/span event + 36 B/stop search + 4 B/stop chunk word (svt_work)"}},
             "index_build": {"index_ms_load": load_stats["index_ms"], "load_ms": load_stats,
-                            "value_index_resident": round(n_total / (refine_ms * 1e-3), 1),
+                            "value_index_resident": round((n if args.emulate_shard else n_total) / (refine_ms * 1e-3), 1),
                             "note": "value_index_resident: loci/s of the refine launch alone, the index built once "
                                     "(BAI-like amortisation); not the headline"},
             "cpu_baseline": cpu,

@@ -269,19 +269,19 @@ uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
 typedef struct svt_load_stats {
     double host_ms;      /* host pass: validation, prefix-max endpos, records, buckets, ranges  */
     double upload_ms;    /* synchronous H2D copies of the caller's arrays (CIGAR words incl.)    */
-    double index_ms;     /* device index build: census + range scan + emit kernels (HIP events)  */
+    double index_ms;     /* device index build: census (+ look-back scan) and emit kernels       */
     double total_ms;     /* wall time of the whole svt_load_pileup call                          */
     uint64_t index_bytes;   /* algorithmic bytes one index build moves: the CIGAR stream twice
-                               (4 B/op), per read 24 B read + 12 B written per pass and its 32 B of
-                               offsets, 16 B per span event, 144 B per 32-op lead arena block   */
+                               (4 B/op), per read 24 B read per pass + its rec word + its 32 B of
+                               offsets, 16 B per span event, 16 B per lead chunk unit          */
     uint64_t span_events;   /* D-list + I-list span events of the pileup                         */
-    uint64_t lead_blocks;   /* 32-op lead arena blocks (leading-S reads)                         */
+    uint64_t lead_blocks;   /* 16-B lead chunk units (leading-S reads: header + 4 words / 32 ops) */
     uint64_t slow_reads;    /* reads whose walk reaches 2^28 bases or position 2^29              */
 } svt_load_stats;
 svt_status svt_last_load_stats(const svt_ctx *ctx, svt_load_stats *out);
 
 /* Rebuild the device index from the resident pileup on `hip_stream` (asynchronous, ordered
- * after every launch of the context already issued): the same three kernels svt_load_pileup
+ * after every launch of the context already issued): the same two kernels svt_load_pileup
  * runs, no host work and no transfers.  Results of later refines are unchanged; bench.py
  * times it as part of every step so that the step covers the whole per-read walk. */
 svt_status svt_reindex(svt_ctx *ctx, void *hip_stream);

@@ -34,6 +34,7 @@
 #include <chrono>
 #include <new>
 #include <atomic>
+#include <type_traits>
 #include <thread>
 #include <vector>
 
@@ -53,18 +54,19 @@ constexpr int BKT_SHIFT = 12;               // read-start bucket = 4096 bp
 constexpr uint32_t NCIG_MASK = 0x1fffffffu; // rec.z: n_cigar | slow << 29 | clip << 30
 constexpr uint32_t SLOW_BIT = 1u << 29;
 constexpr uint32_t STREAM_PAD = 1024;       // zero words after the CIGAR stream (index_kernel's slot over-read)
-// Lead arena (refine_end's stop searches, refinement.c:210-221): the CIGAR of every read whose
-// first op is S (and that is not slow), copied to a 32-op-aligned block, with a chunk index of
-// one word per CHUNK ops: the walk position after the chunk's last op (refinement.c:141).
+// Lead chunks (refine_end's stop searches, refinement.c:210-221): for every read whose first op
+// is S (and that is not slow), a 16-B header {stream offset, n_cigar} and a chunk index of one
+// word per CHUNK ops -- the walk position after the chunk's last op (refinement.c:141) -- in
+// 16-B units; the read's SP_LEAD event carries its header's unit index.
 constexpr int CHUNK = 8;                    // ops per chunk
-constexpr int ALIGN_OPS = 32;               // lead arena block: 4 chunk words = one 16-B load
+constexpr int ALIGN_OPS = 32;               // ops per lead unit (4 chunk words = one 16-B load)
 constexpr uint32_t CH_POS = 0x1fffffffu;    // chunk word: walk position after the chunk's last op
-constexpr uint32_t LEAD_PAD = 64;           // zero words after the lead arena / its chunk index
+constexpr uint32_t LEAD_PAD = 64;           // zero words after the lead chunks
 constexpr uint64_t INDEX_LIMIT = 1ull << 29; // walks reaching position 2^29 are flagged slow
 constexpr uint64_t WALK_LIMIT = 1ull << 28;  // ... and so are walks of 2^28 bases or more (a span event's 28-bit field)
 // Span events (svt_load_pileup, index_kernel<true>): every read's breakpoint events, 16 B each,
 // self-contained {x, w, endpos, aux} so that a window is one filter over a contiguous span:
-//   D list: SP_LEAD {pos, walk << 4 | SP_LEAD, endpos, lead arena block} for cigar[0] == S (:210),
+//   D list: SP_LEAD {pos, walk << 4 | SP_LEAD, endpos, lead unit} for cigar[0] == S (:210),
 //           D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:190),
 //           SP_TRAIL {walk end, SP_TRAIL, endpos, 0} for cigar[n-1] == S (:120,:147);
 //   I list: I >= 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:299).
@@ -79,9 +81,9 @@ struct DevPileup {
     const int64_t *bkt_off;   // [n_targets+1] start of each contig's bucket table
     const uint2 *bkt;         // {first read with pos >= b << BKT_SHIFT, first read with emax >= b << BKT_SHIFT}
     const uint32_t *cigar;    // the CIGAR stream (caller's words; one 0M word for n_cigar == 0 reads)
-    const uint32_t *lcig;     // lead arena (32-op blocks)
-    const uint32_t *lchunk;   // its chunk index (CH_POS words, 4 per block)
-    const uint2 *rec2;        // [n_reads] {walk end, candidate ops (D > 50 + I >= 50)}
+    const uint32_t *lchunk;   // lead chunks: per leading-S read a 16-B header {stream offset, n_cigar}
+                              // and its chunk index (the walk position after every CHUNK ops, CH_POS)
+    const uint64_t *insbase;  // [n_reads+1] I >= 50 ops before read r (every read)
     const uint64_t *spoffD;   // [n_reads+1] span events: read r's D-list events are spD[spoffD[r] .. spoffD[r+1])
     const uint64_t *spoffI;   // [n_reads+1]              its I-list events spI[spoffI[r] .. spoffI[r+1])
     const uint4 *spD;
@@ -377,13 +379,19 @@ __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141:
 #endif
 
 
+// A lead read's CIGAR in the stream: its header's offset (lead unit u).
+__device__ __forceinline__ uint64_t lead_soff(const DevPileup &P, uint64_t u) {
+    const uint2 h = *reinterpret_cast<const uint2 *>(P.lchunk + u * 4u);
+    return (uint64_t)h.x | (uint64_t)h.y << 32;
+}
+
 // Walk position after the break op of a leading-S read that breaks (walk end > e): the first
-// op whose walk position after it exceeds e, from the read's lead arena block at op0.
+// op whose walk position after it exceeds e, from the read's lead chunks (first unit u).
 // Wave-cooperative, uniform arguments; `op_idx` receives the break op's index in the read.
-__device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0, uint32_t ncig, uint32_t rpos,
+__device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t u, uint32_t ncig, uint32_t rpos,
                                                 uint32_t e, uint32_t &op_idx) {
     const int ln = lane_id();
-    const uint64_t c0 = op0 / CHUNK;
+    const uint64_t c0 = (u + 1u) * 4u;
     const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
     uint32_t bc = nch, before = rpos;   // break chunk, walk position before it
     for (uint32_t b = 0; b < nch; b += 4 * WAVE) {
@@ -409,7 +417,7 @@ __device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t op0
         before = rdlane(E[3], WAVE - 1);   // chunk b + 4*64 - 1 ends here (all <= e)
     }
     // the break op inside chunk bc: lanes 0-7 take its ops
-    const uint32_t w = ln < CHUNK ? P.lcig[op0 + (uint64_t)bc * CHUNK + (uint32_t)ln] : 0u;
+    const uint32_t w = ln < CHUNK ? P.cigar[lead_soff(P, u) + (uint64_t)bc * CHUNK + (uint32_t)ln] : 0u;
     const uint32_t after = before + wave_scan_add(ln < CHUNK ? ref_adv(w) : 0u);
     const uint64_t m = ballot(ln < CHUNK && after > e);
     const int k = __builtin_ctzll(m);   // exists: the chunk ends past e
@@ -438,8 +446,7 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t m, ui
     const uint32_t ncig = (uint32_t)__shfl((int)ncig_v, has ? my : 0, WAVE);
     const uint32_t rpos = (uint32_t)__shfl((int)rpos_v, has ? my : 0, WAVE);
     const uint32_t blk = (uint32_t)__shfl((int)blk_v, has ? my : 0, WAVE);
-    const uint64_t op0 = has ? (uint64_t)blk * ALIGN_OPS : 0ull;
-    const uint64_t c0 = op0 / CHUNK;
+    const uint64_t c0 = ((uint64_t)blk + 1u) * 4u;   // the read's chunk words (after its header)
     const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
     bool found = false;
     uint32_t bc = 0;
@@ -462,7 +469,7 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t m, ui
         if (!ballot(has && !found && it + 64 < nch)) break;
     }
     // the break chunk's ops (row lanes 0-7) and the walk position before it (row lane 8)
-    const uint32_t w = has && t < CHUNK ? P.lcig[op0 + (uint64_t)bc * CHUNK + (uint32_t)t] : 0u;
+    const uint32_t w = has && t < CHUNK ? P.cigar[lead_soff(P, blk) + (uint64_t)bc * CHUNK + (uint32_t)t] : 0u;
     const uint32_t pv = has && t == CHUNK ? (bc ? P.lchunk[c0 + bc - 1] & CH_POS : rpos) : 0u;
     const uint32_t before = (uint32_t)__shfl((int)pv, 16 * g + CHUNK, WAVE);
     uint32_t x = t < CHUNK ? ref_adv(w) : 0u;
@@ -517,7 +524,7 @@ __device__ __forceinline__ void span_count(const DevPileup &P, int tid, uint32_t
             const int l = __builtin_ctzll(m);
             m &= m - 1;
             uint32_t bi;
-            (void)break_after(P, (uint64_t)rdlane(v.w, l) * ALIGN_OPS, NCIG_MASK, rdlane(v.x, l), e, bi);
+            (void)break_after(P, (uint64_t)rdlane(v.w, l), NCIG_MASK, rdlane(v.x, l), e, bi);
             st.stops++;
             st.stopch += (unsigned long long)(bi / CHUNK + 1u);
         }
@@ -572,7 +579,7 @@ __device__ __forceinline__ bool span_query(const DevPileup &P, int tid, int64_t 
 // A refine_end stop search deferred by the lane kernel: the breaking read's arena offset / 32,
 // its pos, the window end, the window (searched later for a whole chunk of windows at once).
 struct StopReq {
-    uint32_t op32, rpos, e, kw;
+    uint32_t op32, rpos, e, kw;   // the read's lead unit, its pos, the window end, the window
 };
 struct StopList {
     StopReq *q;
@@ -1627,7 +1634,8 @@ __device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &l
 // position after every 8 arena ops; the read's chunks are scanned 4 at a time (its first
 // chunk is 4-chunk aligned: reads start on 32-op boundaries), then the break chunk's 8 ops.
 __device__ __forceinline__ uint32_t stop_lane(const DevPileup &P, const StopReq &r) {
-    const uint64_t op0 = (uint64_t)r.op32 * ALIGN_OPS, c0 = op0 / CHUNK;
+    const uint64_t c0 = ((uint64_t)r.op32 + 1u) * 4u;      // the read's chunk words (after its header)
+    const uint64_t so = lead_soff(P, r.op32);               // its CIGAR in the stream (loaded alongside)
     uint32_t prev = r.rpos, bc = 0, before = r.rpos;
     for (uint32_t c = 0;; c += 4) {   // the break exists (walk end > e): the scan ends inside the read
         const uint4 q = *reinterpret_cast<const uint4 *>(P.lchunk + c0 + c);
@@ -1643,9 +1651,10 @@ __device__ __forceinline__ uint32_t stop_lane(const DevPileup &P, const StopReq 
         }
         prev = E[3];
     }
-    const uint4 *cw = reinterpret_cast<const uint4 *>(P.lcig + op0 + (uint64_t)bc * CHUNK);
-    const uint4 w0 = cw[0], w1 = cw[1];
-    const uint32_t W[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    const uint32_t *cw = P.cigar + so + (uint64_t)bc * CHUNK;   // the break chunk's ops (any alignment)
+    uint32_t W[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) W[i] = cw[i];
     uint32_t after = before, res = 0;
     bool found = false;
 #pragma unroll
@@ -1962,15 +1971,16 @@ struct svt_ctx {
     int64_t *d_tid_off = nullptr, *d_bkt_off = nullptr;
     uint2 *d_bkt = nullptr;
     uint32_t *d_cigar = nullptr;      // CIGAR stream
-    uint2 *d_rec2 = nullptr;
     uint64_t *d_insbase = nullptr;    // per read: its first I >= 50 op's index in the insertion sequences
     uint64_t n_ins = 0;               // I >= 50 ops in the pileup
     // device index (svt_index.inc)
     uint64_t *d_part = nullptr;       // [n_ranges + 1]
     uint32_t n_ranges = 0;
-    uint32_t *d_wtot = nullptr;
-    uint64_t *d_wbase = nullptr, *d_tot = nullptr;
-    uint32_t *d_lcig = nullptr, *d_lchunk = nullptr;
+    IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan
+    uint64_t *d_tot = nullptr;
+    void *d_scan_tmp = nullptr;       // hipcub scan scratch
+    size_t scan_tmp_bytes = 0;
+    uint32_t *d_lchunk = nullptr;
     uint64_t n_evD = 0, n_evI = 0, n_slow = 0, n_lead_blocks = 0;
     // allele-consensus mode (svt_load_insseq / svt_poa_consensus)
     uint64_t *d_ins_off = nullptr;
@@ -2072,8 +2082,10 @@ svt_status grow_pool(svt_ctx *c) {
 void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
-    hfree(c->d_rec2); hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_wtot); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_lcig); hfree(c->d_lchunk);
+    hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
+    hfree(c->d_part); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
+    hfree(c->d_lchunk);
+    c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
     c->n_evD = c->n_evI = c->n_slow = c->n_lead_blocks = 0;
@@ -2083,7 +2095,7 @@ void free_pileup(svt_ctx *c) {
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
-                       c->d_cigar, c->d_lcig, c->d_lchunk, c->d_rec2, c->d_spoffD, c->d_spoffI,
+                       c->d_cigar, c->d_lchunk, c->d_insbase, c->d_spoffD, c->d_spoffI,
                        c->d_spD, c->d_spI, c->d_slowpre, c->n_targets};
     a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
                     c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
@@ -2410,23 +2422,26 @@ void parallel_for(size_t n, size_t cap, F fn) {
     for (auto &x : th) x.join();
 }
 
-// The device index of the loaded pileup (svt_index.inc): census, scan of the range totals, emit.
-// `first`: size and allocate the event lists and the lead arena from the totals (one synchronous
-// read-back); later calls (svt_reindex) reuse them -- the totals depend on the pileup only.
-// `ms`: the index kernels' device time (HIP events; the read-back and allocations excluded).
+// The device index of the loaded pileup (svt_index.inc): census (with the ranges' look-back
+// scan), then emit.  `first`: size and allocate the event lists and the lead chunks from the
+// totals (one synchronous read-back); later calls (svt_reindex) reuse them -- the totals depend
+// on the pileup only.  `ms`: the index kernels' device time (HIP events; the read-back and
+// allocations excluded).
 svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     IxArgs a;
     a.stream = c->d_cigar;
     a.soff = c->d_off64;
     a.rec = c->d_rec;
-    a.rec2 = c->d_rec2;
     a.part = c->d_part;
-    a.wtot = c->d_wtot;
+    a.agg = c->d_agg;
     a.wbase = c->d_wbase;
     a.spoffD = c->d_spoffD;
     a.spoffI = c->d_spoffI;
     a.insbase = c->d_insbase;
     a.slowpre = c->d_slowpre;
+    a.spD = c->d_spD;
+    a.spI = c->d_spI;
+    a.lchunk = c->d_lchunk;
     a.n_ranges = c->n_ranges;
     const dim3 grid((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block(64 * IX_WPB);
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -2439,10 +2454,16 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     };
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     hipLaunchKernelGGL(index_kernel<false>, grid, block, 0, st, a);
-    hipLaunchKernelGGL(range_scan_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t *)c->d_wtot, c->d_wbase,
-                       c->n_ranges, c->d_tot, c->d_spoffD, c->d_spoffI, c->d_insbase, c->d_slowpre,
-                       (uint64_t)c->n_reads);
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess)   // the ranges' exclusive prefixes
+        e = hipcub::DeviceScan::ExclusiveScan(c->d_scan_tmp, c->scan_tmp_bytes, c->d_agg, c->d_wbase, IxTotSum(),
+                                              IxTot{}, (int)c->n_ranges, st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(ix_totals_kernel, dim3(1), dim3(64), 0, st, (const IxTot *)c->d_agg,
+                           (const IxTot *)c->d_wbase, c->n_ranges, c->d_tot, c->d_spoffD, c->d_spoffI, c->d_insbase,
+                           c->d_slowpre, (uint64_t)c->n_reads);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index census: %s", hipGetErrorString(e)));
     if (ms && hipEventRecord(ev[1], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     if (first) {
@@ -2455,19 +2476,16 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
         c->n_ins = t[IX_INS];
         c->n_slow = t[IX_SLOW];
         c->n_lead_blocks = t[IX_LB];
-        if (c->n_lead_blocks >= (1ull << 32))   // a lead event's block index is 32 bits
-            return done(fail(c, SVT_EINVAL, "pileup: %s", ">= 2^32 lead arena blocks (2^37 leading-S CIGAR ops)"));
-        const uint64_t lw = c->n_lead_blocks * ALIGN_OPS + LEAD_PAD, cw = c->n_lead_blocks * (ALIGN_OPS / CHUNK) + LEAD_PAD;
+        if (c->n_lead_blocks >= (1ull << 32))   // a lead event's unit index is 32 bits
+            return done(fail(c, SVT_EINVAL, "pileup: %s", ">= 2^32 lead chunk units (2^37 leading-S CIGAR ops)"));
         svt_status s;
         if ((s = upload<uint4>(c, c->d_spD, nullptr, 0, std::max<uint64_t>(c->n_evD, 1)))) return done(s);
         if ((s = upload<uint4>(c, c->d_spI, nullptr, 0, std::max<uint64_t>(c->n_evI, 1)))) return done(s);
-        if ((s = upload<uint32_t>(c, c->d_lcig, nullptr, 0, lw))) return done(s);
-        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, cw))) return done(s);
+        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, c->n_lead_blocks * 4u + LEAD_PAD))) return done(s);
+        a.spD = c->d_spD;
+        a.spI = c->d_spI;
+        a.lchunk = c->d_lchunk;
     }
-    a.spD = c->d_spD;
-    a.spI = c->d_spI;
-    a.lcig = c->d_lcig;
-    a.lchunk = c->d_lchunk;
     if (ms && hipEventRecord(ev[2], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     hipLaunchKernelGGL(index_kernel<true>, grid, block, 0, st, a);
     e = hipGetLastError();
@@ -2608,13 +2626,22 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload(c, c->d_cigar, strm, (size_t)nstream, STREAM_PAD))) return s;
     if ((s = upload(c, c->d_part, part.data(), part.size()))) return s;
     const size_t S = (size_t)nr + 1;
-    if ((s = upload<uint2>(c, c->d_rec2, nullptr, 0, std::max<size_t>((size_t)nr, 1)))) return s;
     if ((s = upload<uint64_t>(c, c->d_spoffD, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_spoffI, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, S))) return s;
-    if ((s = upload<uint32_t>(c, c->d_wtot, nullptr, 0, std::max<size_t>((size_t)c->n_ranges, 1) * IX_NTOT))) return s;
-    if ((s = upload<uint64_t>(c, c->d_wbase, nullptr, 0, std::max<size_t>((size_t)c->n_ranges, 1) * IX_NTOT))) return s;
+    const size_t NR = std::max<size_t>((size_t)c->n_ranges, 1);
+    if ((s = upload<IxTot>(c, c->d_agg, nullptr, 0, NR))) return s;
+    if ((s = upload<IxTot>(c, c->d_wbase, nullptr, 0, NR))) return s;
+    if (c->n_ranges > 0x7fffffffu) return fail(c, SVT_EINVAL, "pileup: %s", "too many index ranges");
+    {
+        size_t need = 0;
+        HIP_TRY(c, hipcub::DeviceScan::ExclusiveScan(nullptr, need, c->d_agg, c->d_wbase, IxTotSum(), IxTot{},
+                                                     (int)c->n_ranges, (hipStream_t)nullptr));
+        if ((s = upload<unsigned char>(c, reinterpret_cast<unsigned char *&>(c->d_scan_tmp), nullptr, 0,
+                                       std::max<size_t>(need, 1)))) return s;
+        c->scan_tmp_bytes = std::max<size_t>(need, 1);
+    }
     if ((s = upload<uint64_t>(c, c->d_tot, nullptr, 0, IX_NTOT))) return s;
     c->load_stats.upload_ms = ms_since(t_up);
     c->n_targets = nt;
@@ -2628,13 +2655,12 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         c->load_stats.span_events = c->n_evD + c->n_evI;
         c->load_stats.lead_blocks = c->n_lead_blocks;
         c->load_stats.slow_reads = c->n_slow;
-        c->load_stats.index_bytes = 8ull * nstream + 2ull * (24ull + 12ull) * R + 32ull * R +
-                                    16ull * (c->n_evD + c->n_evI) + 144ull * c->n_lead_blocks;
+        c->load_stats.index_bytes = 8ull * nstream + 2ull * 24ull * R + 4ull * R + 32ull * R +
+                                    16ull * (c->n_evD + c->n_evI) + 16ull * c->n_lead_blocks;
     } else {
         for (auto *pp : {&c->d_spD, &c->d_spI})
             if ((s = upload<uint4>(c, *pp, nullptr, 0, 1))) return s;
-        for (auto *pp : {&c->d_lcig, &c->d_lchunk})
-            if ((s = upload<uint32_t>(c, *pp, nullptr, 0, LEAD_PAD))) return s;
+        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, LEAD_PAD))) return s;
     }
     HIP_TRY(c, hipDeviceSynchronize());
     c->loaded = true;

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Run ON THE GPU BOX: kernel throughput on the other BASELINE workloads (the headline cfg4 line
-# is bench.py's default).  Each step has its own time limit; stops at the first failure.
-#   tools/gpu_configs.sh TAG
+# Run ON THE GPU BOX: the other BASELINE workloads (the headline cfg4 line is bench.py's
+# default) and the per-rank work of the 8-GPU run, one time limit per step; stops at the
+# first failure.   tools/gpu_configs.sh TAG
 set -u
 TAG=${1:?tag}
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -14,9 +14,11 @@ run() {  # name, timeout, args...
   local rc=$?
   echo "[$(date +%T)] $name rc=$rc" >> "$OUT/steps.log"
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
-  tail -1 "$OUT/$name.log"
+  tail -1 "$OUT/$name.log" | cut -c1-400
 }
-run cfg2 300 --workload cfg2_10kdel_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
+run cfg4_shard8_r0 300 --emulate-shard 8:0 --steps 20 --warmup 3 --no-cpu-baseline
+run cfg4_shard8_r7 300 --emulate-shard 8:7 --steps 20 --warmup 3 --no-cpu-baseline
+run cfg4_scale0125 300 --scale 0.125 --steps 20 --warmup 3 --no-cpu-baseline
 run cfg3 300 --workload cfg3_50k_delins_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
+run cfg2 300 --workload cfg2_10kdel_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
 run cfg1 200 --workload cfg1_100del_10x --steps 20 --warmup 3 --no-cpu-baseline
-run cfg5q 600 --workload cfg5_100k_60x_ul_ont --scale 0.25 --steps 10 --warmup 2 --no-cpu-baseline

@@ -35,7 +35,6 @@ def med(v: list[float]) -> float | None:
 
 STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's kernel name)
     "index_kernel<census>": "index_kernel<false>",
-    "range_scan_kernel": "range_scan_kernel",
     "index_kernel<emit>": "index_kernel<true>",
     "refine_lane_kernel": "refine_lane_kernel",
     "refine_redo_kernel": "refine_redo_kernel",
