@@ -22,3 +22,4 @@ run cfg4_scale0125 300 --scale 0.125 --steps 20 --warmup 3 --no-cpu-baseline
 run cfg3 300 --workload cfg3_50k_delins_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
 run cfg2 300 --workload cfg2_10kdel_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
 run cfg1 200 --workload cfg1_100del_10x --steps 20 --warmup 3 --no-cpu-baseline
+run cfg5 900 --workload cfg5_100k_60x_ul_ont --steps 10 --warmup 2 --no-cpu-baseline
