@@ -2000,7 +2000,8 @@ struct svt_ctx {
     // spill pool + status + work counters
     int32_t *d_pool = nullptr;
     unsigned long long pool_words = 0;
-    unsigned char *d_ctl = nullptr;   // [0,8) pool head (epoch-tagged), [8,12) sticky status, [16,16+8*W_N) work
+    unsigned char *d_ctl = nullptr;   // [0,8) pool head (epoch-tagged), [8,12) sticky status, [12,16) index
+                                      // build guard, [16,16+8*W_N) work, [CTL_REDO, +8) left-over counters
     uint32_t epoch = 0;               // launches so far (pool epochs cycle through 1 .. 2^24-1)
     // launches run in submission order across streams (order_on)
     hipStream_t last_stream = nullptr;
@@ -2442,6 +2443,10 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.spD = c->d_spD;
     a.spI = c->d_spI;
     a.lchunk = c->d_lchunk;
+    a.capD = c->n_evD;
+    a.capI = c->n_evI;
+    a.capL = c->n_lead_blocks * 4u;
+    a.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
     a.n_ranges = c->n_ranges;
     const dim3 grid((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block(64 * IX_WPB);
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -2485,6 +2490,9 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
         a.spD = c->d_spD;
         a.spI = c->d_spI;
         a.lchunk = c->d_lchunk;
+        a.capD = c->n_evD;
+        a.capI = c->n_evI;
+        a.capL = c->n_lead_blocks * 4u;
     }
     if (ms && hipEventRecord(ev[2], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     hipLaunchKernelGGL(index_kernel<true>, grid, block, 0, st, a);
@@ -2663,6 +2671,14 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, LEAD_PAD))) return s;
     }
     HIP_TRY(c, hipDeviceSynchronize());
+    {
+        uint32_t ixerr = 0;
+        HIP_TRY(c, hipMemcpy(&ixerr, c->d_ctl + 12, 4, hipMemcpyDeviceToHost));
+        if (ixerr) {
+            HIP_TRY(c, hipMemset(c->d_ctl + 12, 0, 4));
+            return fail(c, SVT_EDEVICE, "%s", "device index build: emit overran the census's sizes");
+        }
+    }
     c->loaded = true;
     c->load_stats.total_ms = ms_since(t_start);
     return SVT_OK;
@@ -2742,8 +2758,13 @@ svt_status svt_sync(svt_ctx *c, void *stream) {
     DEV_GUARD(c);
     HIP_TRY(c, hipStreamSynchronize((hipStream_t)stream));
     if (c->have_last && c->last_stream != (hipStream_t)stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
-    int32_t status = 0;
-    HIP_TRY(c, hipMemcpy(&status, c->d_ctl + 8, 4, hipMemcpyDeviceToHost));
+    int32_t st2[2] = {0, 0};
+    HIP_TRY(c, hipMemcpy(st2, c->d_ctl + 8, 8, hipMemcpyDeviceToHost));
+    int32_t status = st2[0];
+    if (st2[1]) {   // the index build's guard fired: census and emit disagreed (an engine bug)
+        HIP_TRY(c, hipMemset(c->d_ctl + 12, 0, 4));
+        return fail(c, SVT_EDEVICE, "%s", "device index build: emit overran the census's sizes (results invalid)");
+    }
 #if SVT_DIAG == 9
     fprintf(stderr, "[diag] wave-wide (phase 3) windows: %d\n", status >> 8);
     HIP_TRY(c, hipMemset(c->d_ctl + 8, 0, 4));

@@ -213,3 +213,45 @@ def test_edge_cases(engine_factory):
     check(eng, pl, loci, off, bases, cap=0)
     n, res = check(eng, pl, loci, off, bases, max_seqs=1)
     assert res["n_used"].max() <= 1
+
+
+@pytest.mark.timeout(900)
+def test_poa_cfg3_workload(engine_factory):
+    """BASELINE config 3's "abPOA consensus path enabled" at size: the allele consensus of every
+    refined INS call of the full 50k-locus cfg3 workload on the GPU, checked against the oracle
+    on the first 12k loci (over 5k INS calls; 16 checker threads).  Parity unpinned: the
+    reference never calls abPOA (Makefile:16)."""
+    from concurrent.futures import ThreadPoolExecutor
+    cfg = sim.WORKLOADS["cfg3_50k_delins_30x_ont"]
+    r = sim.generate(cfg, keep_handle=True)
+    off, bases = sim.insertion_sequences(r, cfg, err_permille=50)
+    eng = engine_factory()
+    try:
+        eng.load_pileup(r.pileup)
+        eng.load_insseq(off, bases)
+        refined = eng.refine(r.loci)
+        res, out = eng.poa_consensus(r.loci, refined, cap=4096)
+        ins = r.loci["type"] == 1
+        done = (res["len"] >= 0)
+        assert (done == (ins & (refined["start"] != SVT_NA))).all()   # every refined INS call, nothing else
+        ib = ins_base_of(r.pileup)
+        prm, pp = eng.params, dict(O.POA_DEFAULTS)
+        sub = [i for i in range(min(12000, len(r.loci))) if done[i]]
+
+        def one(i):
+            l, R = r.loci[i], int(refined["start"][i])
+            s = (int(l["pos"]) - prm.median_interval) & 0xFFFFFFFF
+            e = (int(l["pos"]) + prm.median_interval) & 0xFFFFFFFF
+            idx = O.poa_support(r.pileup, ib, int(l["chrom"]), s, e, R, cap=pp["max_support"])
+            want, used = O.poa_consensus([bases[off[k]:off[k + 1]] for k in idx])
+            ok = (res["n_used"][i] == used and res["len"][i] == len(want) and
+                  np.array_equal(out[i, :min(len(want), 4096)], want[:4096]))
+            return i, ok
+
+        with ThreadPoolExecutor(16) as ex:
+            bad = [i for i, ok in ex.map(one, sub) if not ok]
+        assert not bad, f"{len(bad)} of {len(sub)} INS consensus differ, first locus {bad[0]}"
+        assert len(sub) >= 5000
+        print(f"cfg3 POA: {int(done.sum())} INS consensus on the GPU, {len(sub)} checked", file=sys.stderr)
+    finally:
+        eng.close()

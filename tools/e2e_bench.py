@@ -5,6 +5,7 @@ Writes the workload's BAM (+ plain VCF) once, then times the drop-in CLI
 + printing.  Prints one JSON line.
 
     python tools/e2e_bench.py [--workload cfg2_10kdel_30x_ont] [--with-seq] [-t 16] [--reps 3]
+    python tools/e2e_bench.py --workload cfg4_1m_delins_30x_hifi --region-sample 1000   # cpu_baseline's bytes
 """
 from __future__ import annotations
 
@@ -28,15 +29,30 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--level", type=int, default=1, help="BGZF deflate level for the written BAM")
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--region-sample", type=int, default=0, metavar="K",
+                    help="the CPU baseline's sample instead of the whole workload: the first K loci of contig 1 "
+                         "(genomic order) and the BAM of their region, with SEQ/QUAL -- the same bytes bench.py's "
+                         "cpu_baseline BGZF leg times (oracle/bgzf_baseline.py)")
     a = ap.parse_args()
 
-    from svtrek_amd import sim
+    import numpy as np
+
+    from svtrek_amd import Params, sim
     d = a.dir or tempfile.mkdtemp(prefix="svt_e2e_")
     bam, vcf = os.path.join(d, "w.bam"), os.path.join(d, "w.vcf")
     t = time.perf_counter()
     r = sim.generate(sim.WORKLOADS[a.workload], keep_handle=True)
-    sim.write_bam(r, bam, with_seq=a.with_seq, level=a.level)
-    sim.write_vcf(r.loci, vcf)
+    loci, region = r.loci, None
+    if a.region_sample:   # the cpu_baseline sample: same loci, same region, same writer settings
+        prm = Params()
+        c1 = r.loci[r.loci["chrom"] == 1]
+        loci = c1[np.argsort(c1["pos"], kind="stable")][:a.region_sample]
+        w = max(prm.wider_interval, prm.median_interval, prm.narrow_interval)
+        region = (0, max(0, int(loci["pos"].min()) - w - 1), int(max(int(loci["pos"].max()), int(loci["end"].max()))) + w + 1)
+    st = os.statvfs(d)
+    free_gb = st.f_bavail * st.f_frsize / 1e9
+    sim.write_bam(r, bam, with_seq=a.with_seq or bool(a.region_sample), level=a.level, region=region)
+    sim.write_vcf(loci, vcf)
     prep = time.perf_counter() - t
     cli = os.path.join(ROOT, "svtrek_amd", "svtrek")
     times = []
@@ -53,9 +69,11 @@ def main() -> int:
     best = min(times)
     print(json.dumps({
         "metric": "end-to-end svtrek audt (BAM ingest + H2D + refine + print)", "workload": a.workload,
-        "loci": int(len(r.loci)), "printed_records": int(lines), "bam_bytes": os.path.getsize(bam),
-        "with_seq": a.with_seq, "inflate_threads": a.t, "seconds_best": round(best, 3),
-        "seconds_all": [round(x, 3) for x in times], "loci_per_s": round(len(r.loci) / best, 1),
+        "loci": int(len(loci)), "printed_records": int(lines), "bam_bytes": os.path.getsize(bam),
+        "with_seq": a.with_seq or bool(a.region_sample), "inflate_threads": a.t, "seconds_best": round(best, 3),
+        "seconds_all": [round(x, 3) for x in times], "loci_per_s": round(len(loci) / best, 1),
+        "region_sample": {"loci": a.region_sample, "region": region} if a.region_sample else None,
+        "disk_free_gb_before": round(free_gb, 1),
         "prep_seconds": round(prep, 1), "stages_last_run": stages[-1] if stages else None}))
     return 0
 
