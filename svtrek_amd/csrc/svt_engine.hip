@@ -11,7 +11,7 @@
 //      fully coalesced, next tile prefetched while the current one is processed).  A segmented wave prefix scan (DPP) of the reference advance, reset at
 //      each read's first op to its pos, gives every op's walk position at once; because
 //      the walk position only grows inside a read, "this op comes after the break of
-//      refinement.c:145-148" is just `position before the op > inter.end`, so no second
+//      refinement.c:141-144" is just `position before the op > inter.end`, so no second
 //      scan is needed.  Breakpoint candidates (A4-A6) and the soft-clip candidates of
 //      each read's stop op are appended to LDS with LDS atomics; tails of reads that
 //      already broke (and reads that do not overlap the window) are skipped;
@@ -40,7 +40,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.12.0 (gfx950, stream index build, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.13.0 (gfx950, lane-serial index build, span walk, lane vote)"
 
 namespace {
 
@@ -67,7 +67,7 @@ constexpr uint64_t WALK_LIMIT = 1ull << 28;  // ... and so are walks of 2^28 bas
 // Span events (svt_load_pileup, index_kernel<true>): every read's breakpoint events, 16 B each,
 // self-contained {x, w, endpos, aux} so that a window is one filter over a contiguous span:
 //   D list: SP_LEAD {pos, walk << 4 | SP_LEAD, endpos, lead unit} for cigar[0] == S (:210),
-//           D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:190),
+//           D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:188),
 //           SP_TRAIL {walk end, SP_TRAIL, endpos, 0} for cigar[n-1] == S (:120,:147);
 //   I list: I >= 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:299).
 constexpr uint32_t SP_TRAIL = 0xEu, SP_LEAD = 0xFu;   // op codes no candidate event carries
@@ -255,7 +255,7 @@ struct WinStats {
 template <int KIND>
 __device__ __forceinline__ bool is_candidate_op(uint32_t op, uint32_t len) {
     if (KIND == K_INS) return op == OP_INS && (uint32_t)SV_MIN_LENGTH <= len;   // refinement.c:299
-    return op == OP_DEL && (uint32_t)SV_MIN_LENGTH < len;                       // refinement.c:124,:190
+    return op == OP_DEL && (uint32_t)SV_MIN_LENGTH < len;                       // refinement.c:124,:188
 }
 
 // Per-read walk, 64 ops per step, replaying the reference's uint32 position arithmetic
@@ -280,7 +280,7 @@ __device__ __forceinline__ void walk_read(const uint32_t *__restrict__ cigar, ui
         uint64_t bm = ballot(v && after > e);                         // refinement.c:145
         int fb = bm ? __builtin_ctzll(bm) : WAVE;
         bool hit = v && ln <= fb && is_candidate_op<KIND>(op, len);
-        sink.push(hit, KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before);   // :198 / :136
+        sink.push(hit, KIND == K_END ? (int32_t)(before + len + 1u) : (int32_t)before);   // :198 / :134
         if (bm) {
             broke = true;
             stop_rp = rdlane(after, fb);
@@ -610,7 +610,7 @@ __device__ __forceinline__ bool span_cand(const uint4 &v, uint32_t s, uint32_t e
     const uint32_t wend = x + len;
     brk = lead && wend > e;
     val = op == OP_DEL ? x + len + 1u : wend + 1u;
-    return (ovl && x <= e && op == OP_DEL) || (lead && !brk);                  // :190-200
+    return (ovl && x <= e && op == OP_DEL) || (lead && !brk);                  // :188-199
 }
 
 template <int KIND>
@@ -1462,7 +1462,7 @@ __device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, u
     if (KIND == K_START) return ovl & le & (ballot(op == OP_DEL) | (ballot(op == SP_TRAIL) & ballot(s <= x)));
     const uint64_t lead = ovl & le & ballot(op == SP_LEAD) & ballot(s <= x);                    // :210-220
     brk = lead & ballot(x + (v.y >> 4) > e);
-    return (ovl & le & ballot(op == OP_DEL)) | (lead & ~brk);                                   // :190-200
+    return (ovl & le & ballot(op == OP_DEL)) | (lead & ~brk);                                   // :188-199
 }
 
 #ifndef SVT_LW_U
@@ -1982,6 +1982,7 @@ struct svt_ctx {
     size_t scan_tmp_bytes = 0;
     uint32_t *d_lchunk = nullptr;
     uint64_t n_evD = 0, n_evI = 0, n_slow = 0, n_lead_blocks = 0;
+    uint64_t lchunk_units = 0;        // lead chunk area: ix_unit(n_stream, n_reads) + 2 16-B units
     // allele-consensus mode (svt_load_insseq / svt_poa_consensus)
     uint64_t *d_ins_off = nullptr;
     uint8_t *d_ins_bases = nullptr;
@@ -2089,7 +2090,7 @@ void free_pileup(svt_ctx *c) {
     c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
-    c->n_evD = c->n_evI = c->n_slow = c->n_lead_blocks = 0;
+    c->n_evD = c->n_evI = c->n_slow = c->n_lead_blocks = c->lchunk_units = 0;
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
@@ -2445,7 +2446,7 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.lchunk = c->d_lchunk;
     a.capD = c->n_evD;
     a.capI = c->n_evI;
-    a.capL = c->n_lead_blocks * 4u;
+    a.capL = c->lchunk_units * 4u;
     a.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
     a.n_ranges = c->n_ranges;
     const dim3 grid((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block(64 * IX_WPB);
@@ -2481,18 +2482,16 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
         c->n_ins = t[IX_INS];
         c->n_slow = t[IX_SLOW];
         c->n_lead_blocks = t[IX_LB];
-        if (c->n_lead_blocks >= (1ull << 32))   // a lead event's unit index is 32 bits
-            return done(fail(c, SVT_EINVAL, "pileup: %s", ">= 2^32 lead chunk units (2^37 leading-S CIGAR ops)"));
         svt_status s;
         if ((s = upload<uint4>(c, c->d_spD, nullptr, 0, std::max<uint64_t>(c->n_evD, 1)))) return done(s);
         if ((s = upload<uint4>(c, c->d_spI, nullptr, 0, std::max<uint64_t>(c->n_evI, 1)))) return done(s);
-        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, c->n_lead_blocks * 4u + LEAD_PAD))) return done(s);
+        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, c->lchunk_units * 4u + LEAD_PAD))) return done(s);
         a.spD = c->d_spD;
         a.spI = c->d_spI;
         a.lchunk = c->d_lchunk;
         a.capD = c->n_evD;
         a.capI = c->n_evI;
-        a.capL = c->n_lead_blocks * 4u;
+        a.capL = c->lchunk_units * 4u;
     }
     if (ms && hipEventRecord(ev[2], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     hipLaunchKernelGGL(index_kernel<true>, grid, block, 0, st, a);
@@ -2604,6 +2603,9 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         strm = strm2.data();
     }
     const uint64_t nstream = nr > 0 ? soff[nr] : 0;
+    c->lchunk_units = ix_unit(nstream, (uint64_t)nr) + 2u;
+    if (c->lchunk_units >= (1ull << 32))   // a lead event's unit index is 32 bits
+        return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^32 lead chunk units (2^36 stream ops)");
     // ---- ranges of the index build: ~T stream ops each, cut at read starts and contig starts
     const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / 65536, 2048), 1ull << 26);
     std::vector<std::vector<uint64_t>> pt((size_t)nt);
