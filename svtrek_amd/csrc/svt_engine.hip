@@ -125,6 +125,7 @@ constexpr int W_WINDOWS = 0, W_READS = 1, W_OPS = 2, W_CANDS = 3, W_SPILLED = 4,
               W_SPAN = 13, W_N = 14;
 constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status, work counters
 constexpr size_t CTL_REDO = 200;    // two redo counters (alternating launches)
+constexpr size_t CTL_XCNT = 208;    // ranges listed for the exact index census
 static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
 
 // ------------------------------------------------------------------ wave primitives
@@ -1956,6 +1957,7 @@ struct svt_ctx {
     svt_params prm{};
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
+    bool ix_exact = false;        // SVTREK_IX_EXACT=1: every index range takes the exact census (tests)
     int lane_w = 0;               // SVTREK_LANE_W=8|32 forces the lane kernel's windows per wave (A/B)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
@@ -1977,6 +1979,7 @@ struct svt_ctx {
     uint64_t *d_part = nullptr;       // [n_ranges + 1]
     uint32_t n_ranges = 0;
     IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan
+    uint32_t *d_xlist = nullptr;      // [n_ranges] ranges for the exact census
     uint64_t *d_tot = nullptr;
     void *d_scan_tmp = nullptr;       // hipcub scan scratch
     size_t scan_tmp_bytes = 0;
@@ -2085,7 +2088,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
+    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
     hfree(c->d_lchunk);
     c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
@@ -2353,6 +2356,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     c->prm = *params;
     const char *g = getenv("SVTREK_GATHER");   // "span1": the one-wave-per-window kernel at every batch size
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
+    if (const char *x = getenv("SVTREK_IX_EXACT")) c->ix_exact = atoi(x) == 1;
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
@@ -2448,6 +2452,9 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.capI = c->n_evI;
     a.capL = c->lchunk_units * 4u;
     a.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
+    a.xlist = c->d_xlist;
+    a.xcnt = (uint32_t *)(c->d_ctl + CTL_XCNT);
+    a.exact_all = c->ix_exact ? 1u : 0u;
     a.n_ranges = c->n_ranges;
     const dim3 grid((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block(64 * IX_WPB);
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -2459,7 +2466,10 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
         return r;
     };
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
-    hipLaunchKernelGGL(index_kernel<false>, grid, block, 0, st, a);
+    hipLaunchKernelGGL(ix_census_kernel, dim3((unsigned)((c->n_ranges + IXC_WPB - 1) / IXC_WPB)), dim3(64 * IXC_WPB), 0,
+                       st, a);
+    hipLaunchKernelGGL(index_kernel<false>, dim3((unsigned)std::min<uint32_t>(IX_XGRID, (c->n_ranges + IX_WPB - 1) / IX_WPB)),
+                       block, 0, st, a);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess)   // the ranges' exclusive prefixes
         e = hipcub::DeviceScan::ExclusiveScan(c->d_scan_tmp, c->scan_tmp_bytes, c->d_agg, c->d_wbase, IxTotSum(),
@@ -2467,7 +2477,7 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     if (e == hipSuccess) {
         hipLaunchKernelGGL(ix_totals_kernel, dim3(1), dim3(64), 0, st, (const IxTot *)c->d_agg,
                            (const IxTot *)c->d_wbase, c->n_ranges, c->d_tot, c->d_spoffD, c->d_spoffI, c->d_insbase,
-                           c->d_slowpre, (uint64_t)c->n_reads);
+                           c->d_slowpre, (uint64_t)c->n_reads, a.xcnt);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index census: %s", hipGetErrorString(e)));
@@ -2635,6 +2645,7 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
     if ((s = upload(c, c->d_cigar, strm, (size_t)nstream, STREAM_PAD))) return s;
     if ((s = upload(c, c->d_part, part.data(), part.size()))) return s;
+    if ((s = upload<uint32_t>(c, c->d_xlist, nullptr, 0, std::max<size_t>(part.size() - 1, 1)))) return s;
     const size_t S = (size_t)nr + 1;
     if ((s = upload<uint64_t>(c, c->d_spoffD, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_spoffI, nullptr, 0, S))) return s;

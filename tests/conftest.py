@@ -31,18 +31,19 @@ def engine_factory():
     # gather variant -> (SVTREK_GATHER, SVTREK_LANE_W)
     variants = {"span": ("span", "32"), "lane8": ("span", "8"), "auto": ("span", None), "span1": ("span1", None)}
 
-    def make(params=None, gather="span"):
+    def make(params=None, gather="span", env=None):
         """gather: "span" (span events through refine_lane_kernel<32> at every batch size -- the
         product picks it from 64K windows up), "lane8" (refine_lane_kernel<8>), "span1" (one wave per
-        window, refine_span_kernel: the product's pick for smaller batches), "auto" (the product's
-        size-based pick), "event" (candidate-op lists), "index" (chunk-index walk), "stream" (full
-        CIGAR stream) or "perread" (per-read walk) -- the SVTREK_GATHER variants of the engine."""
+        window, refine_span_kernel: the product's pick for smaller batches) or "auto" (the product's
+        size-based pick).  env: extra engine switches read at svt_open (e.g. SVTREK_IX_EXACT=1)."""
         g, lw = variants.get(gather, (gather, None))
-        old = {k: os.environ.get(k) for k in ("SVTREK_GATHER", "SVTREK_LANE_W")}
+        keys = ("SVTREK_GATHER", "SVTREK_LANE_W") + tuple(env or ())
+        old = {k: os.environ.get(k) for k in keys}
         os.environ["SVTREK_GATHER"] = g
         os.environ.pop("SVTREK_LANE_W", None)
         if lw:
             os.environ["SVTREK_LANE_W"] = lw
+        os.environ.update(env or {})
         try:
             e = Engine(params or Params(), device=0)
         finally:

@@ -459,3 +459,40 @@ def test_size_based_kernel_pick_alternating(engine_factory):
     for b, o in zip(seq, outs):
         got = o.cpu().numpy().view(RESULT_DTYPE)
         _assert_same(got, want_b if b is big else want_s, b)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_index_census_streaming_vs_exact(engine_factory, seed):
+    """The index census: ranges whose op lengths cannot reach a slow walk take the streaming
+    reduction, the others the exact per-slot census.  A pileup with slow reads in a few places
+    (so both kinds of range occur), built once as the product does and once with every range
+    forced through the exact census (SVTREK_IX_EXACT=1): same index sizes, same results as the
+    oracle, also after a rebuild from the resident pileup."""
+    from svtrek_amd.pileup import from_reads
+    rng = np.random.default_rng(50 + seed)
+    rows = []
+    big = (1 << 28) - 1
+    pos = 5000
+    for i in range(4000):
+        pos += int(rng.integers(0, 40))
+        n = int(rng.integers(1, 30))
+        ops = [(int(rng.choice([0, 1, 2, 4, 5])), int(rng.integers(1, 120))) for _ in range(n)]
+        if i % 997 == 3:                       # a slow read: its walk passes 2^28
+            ops += [(5, big), (2, 60), (0, 5)]
+        if rng.random() < 0.3:
+            ops = [(4, int(rng.integers(1, 40)))] + ops
+        rows.append((0, pos, ops))
+    pl = from_reads(1, rows)
+    hot = [int(x) for x in rng.integers(6000, pos, size=8)]
+    loci = random_loci(rng, 400, 1, pos + 2000, hot)
+    want = O.refine_batch(pl, loci)
+    stats = []
+    for env in (None, {"SVTREK_IX_EXACT": "1"}):
+        eng = engine_factory(env=env)
+        eng.load_pileup(pl)
+        st = eng.load_stats()
+        stats.append((st["span_events"], st["lead_blocks"], st["slow_reads"]))
+        _assert_same(eng.refine(loci), want, loci)
+        eng.reindex()
+        _assert_same(eng.refine(loci), want, loci)
+    assert stats[0] == stats[1] and stats[0][2] >= 4
