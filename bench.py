@@ -11,9 +11,9 @@ refines the g-th contiguous slice against only the reads its queries can reach
 ("scaling": "strong").
 
 A step is the whole per-locus path from the resident columnar pileup to refined calls:
-  1. the device index build (svt_reindex: index_kernel<census> with a decoupled look-back scan
-     of its ranges, then index_kernel<emit> -- every read's CIGAR walked once,
-     refinement.c:118-159/:184-221/:295-318),
+  1. the device index build (svt_reindex: ix_census_kernel -- a streaming reduction of every
+     range's totals --, a hipcub scan of them, then index_kernel<emit> -- every read's CIGAR
+     walked once, refinement.c:118-159/:184-221/:295-318),
   2. one batched refine launch over the rank's slice (svt_refine_device_records:
      refine_lane_kernel + refine_redo_kernel; loci and 16-B result records resident in HBM),
   3. at N > 1, the one collective of the path: an RCCL gather to rank 0 of the slice's 16-B
@@ -125,7 +125,7 @@ def _engine_version() -> str:
     return version()
 
 
-STEP_KERNELS = ("index_kernel<census>", "index_kernel<emit>", "refine_lane_kernel", "refine_redo_kernel")
+STEP_KERNELS = ("ix_census_kernel", "index_kernel<emit>", "refine_lane_kernel", "refine_redo_kernel")
 
 
 def _traffic(workload: str, kernel: str, records: bool) -> tuple[int | None, str | None]:
@@ -357,9 +357,9 @@ def main() -> int:
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "CIGAR stream twice (4 B/op), 24 B/read read per pass + 4 B/read "
-                                                "rec word + 32 B/read offsets, 16 B/span event, 16 B/lead chunk unit "
-                                                "(svt_load_stats.index_bytes)",
+                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), 16 + 24 B/read read "
+                                                "(census: rec; emit: soff + rec), 32 B/read offsets written, "
+                                                "16 B/span event, 16 B/lead chunk unit (svt_load_stats.index_bytes)",
                          },
                          "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
                                           "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),

@@ -40,7 +40,7 @@
 
 #include "../../include/svtrek_gpu.h"
 
-#define SVT_VERSION "svtrek_amd 0.13.0 (gfx950, lane-serial index build, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.14.0 (gfx950, streaming census + lane-serial emit, span walk, lane vote)"
 
 namespace {
 
@@ -2676,7 +2676,9 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         c->load_stats.span_events = c->n_evD + c->n_evI;
         c->load_stats.lead_blocks = c->n_lead_blocks;
         c->load_stats.slow_reads = c->n_slow;
-        c->load_stats.index_bytes = 8ull * nstream + 2ull * 24ull * R + 4ull * R + 32ull * R +
+        // census: stream + rec (16 B/read); emit: stream + soff + rec (24 B/read), the per-read
+        // offsets written (32 B/read), the events and lead units written
+        c->load_stats.index_bytes = 8ull * nstream + 16ull * R + 24ull * R + 32ull * R +
                                     16ull * (c->n_evD + c->n_evI) + 16ull * c->n_lead_blocks;
     } else {
         for (auto *pp : {&c->d_spD, &c->d_spI})
