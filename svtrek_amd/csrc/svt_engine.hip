@@ -1958,6 +1958,7 @@ struct svt_ctx {
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
     bool ix_exact = false;        // SVTREK_IX_EXACT=1: every index range takes the exact census (tests)
+    uint64_t ix_ranges = 65536;   // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
     int lane_w = 0;               // SVTREK_LANE_W=8|32 forces the lane kernel's windows per wave (A/B)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
@@ -2357,6 +2358,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     const char *g = getenv("SVTREK_GATHER");   // "span1": the one-wave-per-window kernel at every batch size
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *x = getenv("SVTREK_IX_EXACT")) c->ix_exact = atoi(x) == 1;
+    if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
@@ -2617,7 +2619,7 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if (c->lchunk_units >= (1ull << 32))   // a lead event's unit index is 32 bits
         return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^32 lead chunk units (2^36 stream ops)");
     // ---- ranges of the index build: ~T stream ops each, cut at read starts and contig starts
-    const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / 65536, 2048), 1ull << 26);
+    const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / c->ix_ranges, 2048), 1ull << 26);
     std::vector<std::vector<uint64_t>> pt((size_t)nt);
     parallel_for((size_t)nt, 16, [&](size_t t) {
         for (int64_t r = p->tid_off[t], r1 = p->tid_off[t + 1]; r < r1;) {
