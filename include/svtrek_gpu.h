@@ -269,11 +269,12 @@ uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
 typedef struct svt_load_stats {
     double host_ms;      /* host pass: validation, prefix-max endpos, records, buckets, ranges  */
     double upload_ms;    /* synchronous H2D copies of the caller's arrays (CIGAR words incl.)    */
-    double index_ms;     /* device index build: census (+ look-back scan) and emit kernels       */
+    double index_ms;     /* device index build: census, scan of the range totals, emit kernels   */
     double total_ms;     /* wall time of the whole svt_load_pileup call                          */
     uint64_t index_bytes;   /* algorithmic bytes one index build moves: the CIGAR stream twice
-                               (4 B/op), per read 24 B read per pass + its rec word + its 32 B of
-                               offsets, 16 B per span event, 16 B per lead chunk unit          */
+                               (4 B/op: census, emit), per read 16 B (census) + 24 B (emit) read
+                               and 32 B of offsets written, 16 B per span event, 16 B per lead
+                               chunk unit                                                     */
     uint64_t span_events;   /* D-list + I-list span events of the pileup                         */
     uint64_t lead_blocks;   /* 16-B lead chunk units (leading-S reads: header + 4 words / 32 ops) */
     uint64_t slow_reads;    /* reads whose walk reaches 2^28 bases or position 2^29              */
@@ -285,6 +286,29 @@ svt_status svt_last_load_stats(const svt_ctx *ctx, svt_load_stats *out);
  * runs, no host work and no transfers.  Results of later refines are unchanged; bench.py
  * times it as part of every step so that the step covers the whole per-read walk. */
 svt_status svt_reindex(svt_ctx *ctx, void *hip_stream);
+
+/* ---- BGZF inflate (the BAM ingest's decompression on the device) ----
+ * One BGZF block of a compressed buffer (SAM spec 4.1): its raw DEFLATE data comp[coff,
+ * coff + clen) inflates to ulen bytes (the block's ISIZE) at out[uoff].  Replaces the inflate
+ * behind htslib's bgzf_read, which the reference reaches through every sam_itr_next ->
+ * bam_read1 (refinement.c:117, :186, :297). */
+typedef struct svt_bgzf_block {
+    uint64_t coff, uoff;
+    uint32_t clen, ulen;
+} svt_bgzf_block;
+/* Inflate n blocks: comp (host, comp_bytes) -> out (host, out_bytes), synchronous.  Every
+ * block must lie inside its buffers (<= 64 KiB each); SVT_EINVAL names the first block whose
+ * data does not inflate to exactly ulen bytes. */
+svt_status svt_bgzf_inflate(svt_ctx *ctx, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
+                            size_t n, uint8_t *out, size_t out_bytes);
+/* The same on device buffers (the block table on the device too; d_comp readable up to 3
+ * bytes past every block's data), asynchronous on hip_stream; svt_bgzf_inflate_status waits
+ * for the stream and reports the first corrupt block (0xffffffff: none). */
+svt_status svt_bgzf_inflate_device(svt_ctx *ctx, const uint8_t *d_comp, const svt_bgzf_block *d_blocks, size_t n,
+                                   uint8_t *d_out, void *hip_stream);
+svt_status svt_bgzf_inflate_status(svt_ctx *ctx, void *hip_stream, uint32_t *bad_block);
+/* Device time (ms, HIP events) of the last svt_bgzf_inflate's kernel. */
+double svt_bgzf_last_inflate_ms(const svt_ctx *ctx);
 
 const char *svt_last_error(const svt_ctx *ctx);
 void        svt_close(svt_ctx *ctx);

@@ -18,6 +18,8 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <zlib.h>
+
 #include "../include/svtrek_gpu.h"
 #include "svtrek_oracle.h"
 
@@ -213,6 +215,49 @@ svt_status svt_last_load_stats(const svt_ctx *c, svt_load_stats *out) {
     memset(out, 0, sizeof *out);
     return SVT_OK;
 }
+/* BGZF inflate with zlib (raw DEFLATE), block by block: the CPU side of svt_bgzf_inflate. */
+static uint32_t cpu_inflate(const uint8_t *comp, const svt_bgzf_block *b, size_t n, uint8_t *out) {
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return 0;
+    uint32_t bad = 0xffffffffu;
+    for (size_t i = 0; i < n && bad == 0xffffffffu; i++) {
+        inflateReset(&zs);
+        zs.next_in = (Bytef *)(comp + b[i].coff);
+        zs.avail_in = b[i].clen;
+        zs.next_out = out + b[i].uoff;
+        zs.avail_out = b[i].ulen;
+        if (inflate(&zs, Z_FINISH) != Z_STREAM_END || zs.total_out != b[i].ulen) bad = (uint32_t)i;
+    }
+    inflateEnd(&zs);
+    return bad;
+}
+static uint32_t cpu_inflate_bad = 0xffffffffu;
+svt_status svt_bgzf_inflate(svt_ctx *c, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *b, size_t n,
+                            uint8_t *out, size_t out_bytes) {
+    if (!c) return SVT_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (b[i].clen > 65536u || b[i].ulen > 65536u || b[i].coff > comp_bytes || b[i].clen > comp_bytes - b[i].coff ||
+            b[i].uoff > out_bytes || b[i].ulen > out_bytes - b[i].uoff)
+            return fail(c, SVT_EINVAL, "BGZF block outside its buffers (or over 64 KiB)");
+    const uint32_t bad = cpu_inflate(comp, b, n, out);
+    return bad == 0xffffffffu ? SVT_OK : fail(c, SVT_EINVAL, "corrupt BGZF block %u (does not inflate to its ISIZE)", bad);
+}
+svt_status svt_bgzf_inflate_device(svt_ctx *c, const uint8_t *d_comp, const svt_bgzf_block *d_blocks, size_t n,
+                                   uint8_t *d_out, void *s) {   /* host memory stands in for device memory here */
+    (void)s;
+    if (!c) return SVT_EINVAL;
+    cpu_inflate_bad = cpu_inflate(d_comp, d_blocks, n, d_out);
+    return SVT_OK;
+}
+svt_status svt_bgzf_inflate_status(svt_ctx *c, void *s, uint32_t *bad) {
+    (void)s;
+    if (!c || !bad) return SVT_EINVAL;
+    *bad = cpu_inflate_bad;
+    return *bad == 0xffffffffu ? SVT_OK : fail(c, SVT_EINVAL, "corrupt BGZF block %u", *bad);
+}
+double svt_bgzf_last_inflate_ms(const svt_ctx *c) { (void)c; return 0.0; }
+
 const char *svt_last_error(const svt_ctx *c) { return c ? c->err : "NULL context"; }
 void svt_close(svt_ctx *c) {
     if (!c) return;

@@ -28,6 +28,7 @@ LOCUS_DTYPE = np.dtype([("type", "<i4"), ("chrom", "<i4"), ("pos", "<u4"), ("end
 RESULT_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4")])
 SW_QUERY_DTYPE = np.dtype([("chrom", "<i4"), ("start", "<u4"), ("end", "<u4")])     # svt_sw_query
 SW_WINDOW_DTYPE = np.dtype([("candidate", "<i4"), ("support", "<i4")])               # svt_sw_window
+BGZF_BLOCK_DTYPE = np.dtype([("coff", "<u8"), ("uoff", "<u8"), ("clen", "<u4"), ("ulen", "<u4")])   # svt_bgzf_block
 RECORD_DTYPE = np.dtype([("index", "<u4"), ("start", "<u4"), ("end", "<u4"), ("pad", "<u4")])   # svt_record
 
 
@@ -108,6 +109,7 @@ ENGINE_SYMBOLS = (
     "svt_poa_default_params", "svt_pileup_ins_count", "svt_load_insseq", "svt_poa_consensus",
     "svt_poa_deferred", "svt_last_load_stats", "svt_open_multi", "svt_device_count",
     "svt_refine_device_records", "svt_reindex",
+    "svt_bgzf_inflate", "svt_bgzf_inflate_device", "svt_bgzf_inflate_status", "svt_bgzf_last_inflate_ms",
 )
 
 _engine = None
@@ -173,7 +175,13 @@ def bind_abi(lib: C.CDLL) -> C.CDLL:
     lib.svt_poa_consensus.argtypes = [P, C.POINTER(SvtPoaParams), P, P, C.c_size_t, C.c_int32, P, P]
     lib.svt_poa_deferred.argtypes = [P]
     lib.svt_poa_deferred.restype = C.c_uint64
-    for name in ("svt_open", "svt_open_multi", "svt_refine_device_records", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
+    lib.svt_bgzf_inflate.argtypes = [P, P, C.c_size_t, P, C.c_size_t, P, C.c_size_t]
+    lib.svt_bgzf_inflate_device.argtypes = [P, P, P, C.c_size_t, P, P]
+    lib.svt_bgzf_inflate_status.argtypes = [P, P, C.POINTER(C.c_uint32)]
+    lib.svt_bgzf_last_inflate_ms.argtypes = [P]
+    lib.svt_bgzf_last_inflate_ms.restype = C.c_double
+    for name in ("svt_bgzf_inflate", "svt_bgzf_inflate_device", "svt_bgzf_inflate_status",
+                 "svt_open", "svt_open_multi", "svt_refine_device_records", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
                  "svt_reindex", "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):
         getattr(lib, name).restype = C.c_int32
     return lib

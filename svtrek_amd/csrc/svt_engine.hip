@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../include/svtrek_gpu.h"
+#include "svt_inflate.h"
 
 #define SVT_VERSION "svtrek_amd 0.14.0 (gfx950, streaming census + lane-serial emit, span walk, lane vote)"
 
@@ -1950,6 +1951,28 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 #include "svt_index.inc"
 #include "svt_poa.inc"
 
+// ------------------------------------------------------------------ BGZF inflate
+// One lane per BGZF block (svt_inflate.h): a BAM's blocks are independent DEFLATE streams of
+// <= 64 KiB output, so a batch of them fills the chip with no cross-lane work.  The primary
+// Huffman tables of the wave's 64 blocks are interleaved in LDS (entry i of lane l at
+// i * 64 + l: conflict-free for any mix of indices), the slow-path arrays and code lengths in
+// a per-lane global scratch slot.  A persistent grid: lane g takes blocks g, g + G, ...
+constexpr int INF_GRID = 4096;   // workgroups (one wave each) at most: <= 262144 scratch slots
+__global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *comp, const svt_bgzf_block *blk, uint32_t n,
+                                                     uint8_t *out, InfSlow *scratch, uint32_t *err) {
+    __shared__ uint16_t tabs[IF_FAST * WAVE];
+    const uint32_t ln = threadIdx.x;
+    const uint32_t g = blockIdx.x * WAVE + ln;
+    const InfFast F(tabs + ln, WAVE);
+    for (uint32_t b = g; b < n; b += gridDim.x * WAVE) {
+        const svt_bgzf_block k = blk[b];
+        const uint64_t a = k.coff & ~3ull;
+        const int rc = inf_block(reinterpret_cast<const uint32_t *>(comp + a), (uint32_t)(k.coff - a), k.clen,
+                                 out + k.uoff, k.ulen, F, scratch[g]);
+        if (rc != INF_OK) atomicMin(err, b);
+    }
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -2014,6 +2037,13 @@ struct svt_ctx {
     hipEvent_t order_ev = nullptr;
     // svt_open_multi: the contexts of devices[1..] (this one drives devices[0])
     std::vector<svt_ctx *> subs;
+    // BGZF inflate (svt_bgzf_inflate): device buffers grown on demand, never shrunk
+    uint8_t *d_infc = nullptr, *d_info = nullptr;
+    svt_bgzf_block *d_infb = nullptr;
+    InfSlow *d_infs = nullptr;
+    uint32_t *d_inferr = nullptr;
+    size_t infc_cap = 0, info_cap = 0, infb_cap = 0;
+    double inf_ms = 0;                // device time of the last svt_bgzf_inflate's kernel
 };
 
 namespace {
@@ -3001,6 +3031,85 @@ uint64_t svt_pileup_device_bytes(const svt_ctx *c) { return c ? c->dev_bytes : 0
 
 uint64_t svt_poa_deferred(const svt_ctx *c) { return c ? c->poa_deferred : 0; }
 
+svt_status svt_bgzf_inflate_device(svt_ctx *c, const uint8_t *d_comp, const svt_bgzf_block *d_blocks, size_t n,
+                                   uint8_t *d_out, void *stream) {
+    if (!c) return SVT_EINVAL;
+    if (n == 0) return SVT_OK;
+    if (!d_comp || !d_blocks || !d_out) return fail(c, SVT_EINVAL, "%s", "null buffer");
+    if (n > 0xfffffffeull) return fail(c, SVT_EINVAL, "%s", "more than 2^32 - 2 blocks in one call");
+    DEV_GUARD(c);
+    const hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = (unsigned)std::min<size_t>((n + WAVE - 1) / WAVE, (size_t)INF_GRID);
+    if (!c->d_infs) HIP_TRY(c, hipMalloc(&c->d_infs, (size_t)INF_GRID * WAVE * sizeof(InfSlow)));
+    if (!c->d_inferr) HIP_TRY(c, hipMalloc(&c->d_inferr, sizeof(uint32_t)));
+    HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, st, d_comp, d_blocks, (uint32_t)n, d_out, c->d_infs,
+                       c->d_inferr);
+    HIP_TRY(c, hipGetLastError());
+    return SVT_OK;
+}
+
+svt_status svt_bgzf_inflate_status(svt_ctx *c, void *stream, uint32_t *bad_block) {
+    if (!c || !bad_block) return SVT_EINVAL;
+    *bad_block = 0xffffffffu;
+    if (!c->d_inferr) return SVT_OK;
+    DEV_GUARD(c);
+    HIP_TRY(c, hipMemcpyAsync(bad_block, c->d_inferr, sizeof(uint32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(c, hipStreamSynchronize((hipStream_t)stream));
+    if (*bad_block != 0xffffffffu) {
+        char m[64];
+        snprintf(m, sizeof m, "%u", *bad_block);
+        return fail(c, SVT_EINVAL, "corrupt BGZF block %s (does not inflate to its ISIZE)", m);
+    }
+    return SVT_OK;
+}
+
+svt_status svt_bgzf_inflate(svt_ctx *c, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks, size_t n,
+                            uint8_t *out, size_t out_bytes) {
+    if (!c) return SVT_EINVAL;
+    if (n == 0) return SVT_OK;
+    if (!comp || !blocks || !out) return fail(c, SVT_EINVAL, "%s", "null buffer");
+    for (size_t i = 0; i < n; i++) {   // every block inside its buffers (the kernel trusts the table)
+        const svt_bgzf_block &k = blocks[i];
+        if (k.clen > 65536u || k.ulen > 65536u || k.coff > comp_bytes || k.clen > comp_bytes - k.coff ||
+            k.uoff > out_bytes || k.ulen > out_bytes - k.uoff)
+            return fail(c, SVT_EINVAL, "%s", "BGZF block outside its buffers (or over 64 KiB)");
+    }
+    DEV_GUARD(c);
+    svt_status s = order_on(c, nullptr);
+    if (s) return s;
+    auto grow = [&](auto *&p, size_t &cap, size_t bytes) -> svt_status {
+        if (bytes <= cap) return SVT_OK;
+        hfree(p);
+        cap = 0;
+        HIP_TRY(c, hipMalloc(&p, bytes));
+        cap = bytes;
+        return SVT_OK;
+    };
+    if ((s = grow(c->d_infc, c->infc_cap, comp_bytes + 16)) || (s = grow(c->d_info, c->info_cap, std::max<size_t>(out_bytes, 1))) ||
+        (s = grow(c->d_infb, c->infb_cap, n * sizeof(svt_bgzf_block))))
+        return s;
+    HIP_TRY(c, hipMemcpy(c->d_infc, comp, comp_bytes, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_infb, blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIP_TRY(c, hipEventCreate(&e0));
+    HIP_TRY(c, hipEventCreate(&e1));
+    (void)hipEventRecord(e0, nullptr);
+    s = svt_bgzf_inflate_device(c, c->d_infc, c->d_infb, n, c->d_info, nullptr);
+    (void)hipEventRecord(e1, nullptr);
+    uint32_t bad = 0;
+    if (s == SVT_OK) s = svt_bgzf_inflate_status(c, nullptr, &bad);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) c->inf_ms = ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (s) return s;
+    HIP_TRY(c, hipMemcpy(out, c->d_info, out_bytes, hipMemcpyDeviceToHost));
+    return SVT_OK;
+}
+
+double svt_bgzf_last_inflate_ms(const svt_ctx *c) { return c ? c->inf_ms : 0.0; }
+
 void svt_close(svt_ctx *c) {
     if (!c) return;
     for (svt_ctx *d : c->subs) svt_close(d);
@@ -3008,6 +3117,7 @@ void svt_close(svt_ctx *c) {
     DevGuard dg(c->device);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     free_pileup(c);
+    hfree(c->d_infc); hfree(c->d_info); hfree(c->d_infb); hfree(c->d_infs); hfree(c->d_inferr);
     hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->d_redo); hfree(c->poa_small.d); hfree(c->poa_big.d);
     delete c;
 }

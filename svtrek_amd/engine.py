@@ -108,6 +108,23 @@ class Engine:
         asynchronous, no host work, results unchanged)."""
         self._check(self.lib.svt_reindex(self._h, C.c_void_p(stream or 0)))
 
+    def bgzf_inflate(self, comp, blocks: np.ndarray, out_bytes: int | None = None) -> np.ndarray:
+        """Inflate BGZF blocks on the device (svt_bgzf_inflate): comp = the compressed bytes,
+        blocks = BGZF_BLOCK_DTYPE rows {coff, uoff, clen, ulen}; returns the uint8 output."""
+        from ._lib import BGZF_BLOCK_DTYPE
+        c = np.ascontiguousarray(np.frombuffer(comp, dtype=np.uint8) if isinstance(comp, (bytes, bytearray)) else comp,
+                                 dtype=np.uint8)
+        b = np.ascontiguousarray(blocks, dtype=BGZF_BLOCK_DTYPE)
+        if out_bytes is None:
+            out_bytes = int((b["uoff"].astype(np.uint64) + b["ulen"]).max()) if len(b) else 0
+        out = np.empty(max(out_bytes, 1), dtype=np.uint8)
+        self._check(self.lib.svt_bgzf_inflate(self._h, c.ctypes.data, c.nbytes, b.ctypes.data, len(b),
+                                              out.ctypes.data, out_bytes))
+        return out[:out_bytes]
+
+    def last_inflate_ms(self) -> float:
+        return float(self.lib.svt_bgzf_last_inflate_ms(self._h))
+
     def sync(self, stream: int | None = None) -> None:
         self._check(self.lib.svt_sync(self._h, C.c_void_p(stream or 0)))
 
