@@ -125,7 +125,7 @@ def _engine_version() -> str:
     return version()
 
 
-STEP_KERNELS = ("ix_census_kernel", "index_kernel<emit>", "refine_lane_kernel", "refine_redo_kernel")
+STEP_KERNELS = ("ix2_census_kernel", "ix2_emit_kernel", "refine_lane_kernel", "refine_redo_kernel")
 
 
 def _traffic(workload: str, kernel: str, records: bool) -> tuple[int | None, str | None]:
@@ -357,9 +357,9 @@ def main() -> int:
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), 16 + 24 B/read read "
-                                                "(census: rec; emit: soff + rec), 32 B/read offsets written, "
-                                                "16 B/span event, 16 B/lead chunk unit (svt_load_stats.index_bytes)",
+                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), per read 24 + 8 B "
+                                                "(census: soff, rec; cnt written) and 32 + 32 B (emit: cnt, soff, rec; "
+                                                "offsets written), 16 B/span event, 16 B/lead chunk unit (svt_load_stats.index_bytes)",
                          },
                          "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
                                           "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),

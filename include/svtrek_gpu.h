@@ -272,9 +272,9 @@ typedef struct svt_load_stats {
     double index_ms;     /* device index build: census, scan of the range totals, emit kernels   */
     double total_ms;     /* wall time of the whole svt_load_pileup call                          */
     uint64_t index_bytes;   /* algorithmic bytes one index build moves: the CIGAR stream twice
-                               (4 B/op: census, emit), per read 16 B (census) + 24 B (emit) read
-                               and 32 B of offsets written, 16 B per span event, 16 B per lead
-                               chunk unit                                                     */
+                               (4 B/op: census, emit), per read 32 B (census: offsets + record
+                               read, counts written) + 64 B (emit: counts, offsets, record read;
+                               list offsets written), 16 B per span event and lead chunk unit */
     uint64_t span_events;   /* D-list + I-list span events of the pileup                         */
     uint64_t lead_blocks;   /* 16-B lead chunk units (leading-S reads: header + 4 words / 32 ops) */
     uint64_t slow_reads;    /* reads whose walk reaches 2^28 bases or position 2^29              */

@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_inflate.h"
 
-#define SVT_VERSION "svtrek_amd 0.14.0 (gfx950, streaming census + lane-serial emit, span walk, lane vote)"
+#define SVT_VERSION "svtrek_amd 0.15.0 (gfx950, lane-per-read index build, span walk, lane vote, BGZF inflate)"
 
 namespace {
 
@@ -1949,6 +1949,7 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 }
 
 #include "svt_index.inc"
+#include "svt_index2.inc"
 #include "svt_poa.inc"
 
 // ------------------------------------------------------------------ BGZF inflate
@@ -2004,6 +2005,9 @@ struct svt_ctx {
     uint32_t n_ranges = 0;
     IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan
     uint32_t *d_xlist = nullptr;      // [n_ranges] ranges for the exact census
+    uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
+    uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
+    bool ix_lane = true;              // index build: lane per read (svt_index2.inc) / stream walk (SVTREK_IX=stream)
     uint64_t *d_tot = nullptr;
     void *d_scan_tmp = nullptr;       // hipcub scan scratch
     size_t scan_tmp_bytes = 0;
@@ -2119,7 +2123,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
+    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
     hfree(c->d_lchunk);
     c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
@@ -2388,6 +2392,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     const char *g = getenv("SVTREK_GATHER");   // "span1": the one-wave-per-window kernel at every batch size
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *x = getenv("SVTREK_IX_EXACT")) c->ix_exact = atoi(x) == 1;
+    if (const char *x = getenv("SVTREK_IX")) c->ix_lane = strcmp(x, "stream") != 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
@@ -2497,18 +2502,27 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
             if (e) (void)hipEventDestroy(e);
         return r;
     };
+    // lane per read (svt_index2.inc) unless a 64-read group is too large for its 32-bit offsets
+    const bool lane = c->ix_lane && c->n_groups > 0;
+    const uint32_t nparts = lane ? c->n_groups : c->n_ranges;   // what the scan runs over
+    Ix2Args a2{a, c->d_cnt, (uint64_t)c->n_reads, c->n_groups};
+    const dim3 grid2((unsigned)((c->n_groups + IX2_WPB - 1) / IX2_WPB)), block2(64 * IX2_WPB);
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
-    hipLaunchKernelGGL(ix_census_kernel, dim3((unsigned)((c->n_ranges + IXC_WPB - 1) / IXC_WPB)), dim3(64 * IXC_WPB), 0,
-                       st, a);
-    hipLaunchKernelGGL(index_kernel<false>, dim3((unsigned)std::min<uint32_t>(IX_XGRID, (c->n_ranges + IX_WPB - 1) / IX_WPB)),
-                       block, 0, st, a);
+    if (lane) {
+        hipLaunchKernelGGL(ix2_census_kernel, grid2, block2, 0, st, a2);
+    } else {
+        hipLaunchKernelGGL(ix_census_kernel, dim3((unsigned)((c->n_ranges + IXC_WPB - 1) / IXC_WPB)), dim3(64 * IXC_WPB), 0,
+                           st, a);
+        hipLaunchKernelGGL(index_kernel<false>, dim3((unsigned)std::min<uint32_t>(IX_XGRID, (c->n_ranges + IX_WPB - 1) / IX_WPB)),
+                           block, 0, st, a);
+    }
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess)   // the ranges' exclusive prefixes
+    if (e == hipSuccess)   // the ranges' / groups' exclusive prefixes
         e = hipcub::DeviceScan::ExclusiveScan(c->d_scan_tmp, c->scan_tmp_bytes, c->d_agg, c->d_wbase, IxTotSum(),
-                                              IxTot{}, (int)c->n_ranges, st);
+                                              IxTot{}, (int)nparts, st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(ix_totals_kernel, dim3(1), dim3(64), 0, st, (const IxTot *)c->d_agg,
-                           (const IxTot *)c->d_wbase, c->n_ranges, c->d_tot, c->d_spoffD, c->d_spoffI, c->d_insbase,
+                           (const IxTot *)c->d_wbase, nparts, c->d_tot, c->d_spoffD, c->d_spoffI, c->d_insbase,
                            c->d_slowpre, (uint64_t)c->n_reads, a.xcnt);
         e = hipGetLastError();
     }
@@ -2534,9 +2548,11 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
         a.capD = c->n_evD;
         a.capI = c->n_evI;
         a.capL = c->lchunk_units * 4u;
+        a2.a = a;
     }
     if (ms && hipEventRecord(ev[2], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
-    hipLaunchKernelGGL(index_kernel<true>, grid, block, 0, st, a);
+    if (lane) hipLaunchKernelGGL(ix2_emit_kernel, grid2, block2, 0, st, a2);
+    else hipLaunchKernelGGL(index_kernel<true>, grid, block, 0, st, a);
     e = hipGetLastError();
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index emit: %s", hipGetErrorString(e)));
     if (ms) {
@@ -2663,6 +2679,11 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     part.push_back((uint64_t)nr);
     if (part.size() - 1 > 0xffffffffull) return fail(c, SVT_EINVAL, "pileup: %s", "too many index ranges");
     c->n_ranges = (uint32_t)(part.size() - 1);
+    // the lane-per-read index's 64-read groups: each group's ops < 2^27, so that its events fit
+    // the 32-bit wave scans and buffer sizes (else the stream walk builds the index)
+    c->n_groups = (uint32_t)((nr + WAVE - 1) / WAVE);
+    for (int64_t g0 = 0; g0 < nr && c->n_groups; g0 += WAVE)
+        if (soff[std::min<int64_t>(g0 + WAVE, nr)] - soff[g0] >= (1ull << 27)) c->n_groups = 0;
     c->load_stats.host_ms = ms_since(t_start);
 
     const clk::time_point t_up = clk::now();
@@ -2683,14 +2704,15 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload<uint64_t>(c, c->d_spoffI, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, S))) return s;
-    const size_t NR = std::max<size_t>((size_t)c->n_ranges, 1);
+    if ((s = upload<uint2>(c, c->d_cnt, nullptr, 0, std::max<size_t>((size_t)nr, 1)))) return s;
+    const size_t NR = std::max<size_t>({(size_t)c->n_ranges, (size_t)c->n_groups, (size_t)1});
     if ((s = upload<IxTot>(c, c->d_agg, nullptr, 0, NR))) return s;
     if ((s = upload<IxTot>(c, c->d_wbase, nullptr, 0, NR))) return s;
     if (c->n_ranges > 0x7fffffffu) return fail(c, SVT_EINVAL, "pileup: %s", "too many index ranges");
     {
         size_t need = 0;
         HIP_TRY(c, hipcub::DeviceScan::ExclusiveScan(nullptr, need, c->d_agg, c->d_wbase, IxTotSum(), IxTot{},
-                                                     (int)c->n_ranges, (hipStream_t)nullptr));
+                                                     (int)NR, (hipStream_t)nullptr));
         if ((s = upload<unsigned char>(c, reinterpret_cast<unsigned char *&>(c->d_scan_tmp), nullptr, 0,
                                        std::max<size_t>(need, 1)))) return s;
         c->scan_tmp_bytes = std::max<size_t>(need, 1);
@@ -2708,9 +2730,10 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         c->load_stats.span_events = c->n_evD + c->n_evI;
         c->load_stats.lead_blocks = c->n_lead_blocks;
         c->load_stats.slow_reads = c->n_slow;
-        // census: stream + rec (16 B/read); emit: stream + soff + rec (24 B/read), the per-read
-        // offsets written (32 B/read), the events and lead units written
-        c->load_stats.index_bytes = 8ull * nstream + 16ull * R + 24ull * R + 32ull * R +
+        // (lane-per-read index) census: stream + soff + rec (24 B/read), cnt written (8 B/read);
+        // emit: cnt + soff + rec (32 B/read) + stream, the per-read offsets (32 B/read), events
+        // and lead units written
+        c->load_stats.index_bytes = 8ull * nstream + 32ull * R + 32ull * R + 32ull * R +
                                     16ull * (c->n_evD + c->n_evI) + 16ull * c->n_lead_blocks;
     } else {
         for (auto *pp : {&c->d_spD, &c->d_spI})

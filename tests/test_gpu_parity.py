@@ -463,11 +463,12 @@ def test_size_based_kernel_pick_alternating(engine_factory):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_index_census_streaming_vs_exact(engine_factory, seed):
-    """The index census: ranges whose op lengths cannot reach a slow walk take the streaming
-    reduction, the others the exact per-slot census.  A pileup with slow reads in a few places
-    (so both kinds of range occur), built once as the product does and once with every range
-    forced through the exact census (SVTREK_IX_EXACT=1): same index sizes, same results as the
-    oracle, also after a rebuild from the resident pileup."""
+    """The three index builds agree: lane per read (the product's), the stream walk
+    (SVTREK_IX=stream: ranges whose op lengths cannot reach a slow walk take the streaming
+    census, the others the exact per-slot census) and the stream walk with every range forced
+    through the exact census (SVTREK_IX_EXACT=1).  A pileup with slow reads in a few places (so
+    both kinds of range occur): same index sizes, same results as the oracle, also after a
+    rebuild from the resident pileup."""
     from svtrek_amd.pileup import from_reads
     rng = np.random.default_rng(50 + seed)
     rows = []
@@ -487,7 +488,7 @@ def test_index_census_streaming_vs_exact(engine_factory, seed):
     loci = random_loci(rng, 400, 1, pos + 2000, hot)
     want = O.refine_batch(pl, loci)
     stats = []
-    for env in (None, {"SVTREK_IX_EXACT": "1"}):
+    for env in (None, {"SVTREK_IX": "stream"}, {"SVTREK_IX": "stream", "SVTREK_IX_EXACT": "1"}):
         eng = engine_factory(env=env)
         eng.load_pileup(pl)
         st = eng.load_stats()
@@ -495,4 +496,4 @@ def test_index_census_streaming_vs_exact(engine_factory, seed):
         _assert_same(eng.refine(loci), want, loci)
         eng.reindex()
         _assert_same(eng.refine(loci), want, loci)
-    assert stats[0] == stats[1] and stats[0][2] >= 4
+    assert stats[0] == stats[1] == stats[2] and stats[0][2] >= 4

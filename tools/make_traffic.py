@@ -33,8 +33,11 @@ def med(v: list[float]) -> float | None:
     return statistics.median(v) if v else None
 
 
-STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's kernel name)
-    "index_kernel<census>": "index_kernel<false>",
+STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's kernel name); the
+           # index build is either the lane-per-read pair (default) or the stream walk (SVTREK_IX=stream)
+    "ix2_census_kernel": "ix2_census_kernel",
+    "ix2_emit_kernel": "ix2_emit_kernel",
+    "ix_census_kernel": "(anonymous namespace)::ix_census_kernel",
     "index_kernel<emit>": "index_kernel<true>",
     "refine_lane_kernel": "refine_lane_kernel",
     "refine_redo_kernel": "refine_redo_kernel",
