@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <future>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -70,23 +71,165 @@ const Inflater &inflater() {
     return inf;
 }
 
+// Growable byte buffer without value-initialisation; adopt() takes over a malloc'ed block (the
+// device-inflated batches are handed over without a copy).
+struct Bytes {
+    uint8_t *p = nullptr;
+    size_t n = 0, cap = 0;
+    Bytes() = default;
+    Bytes(const Bytes &) = delete;
+    Bytes &operator=(const Bytes &) = delete;
+    ~Bytes() { free(p); }
+    size_t size() const { return n; }
+    uint8_t *data() { return p; }
+    const uint8_t *data() const { return p; }
+    bool resize(size_t m) {
+        if (m > cap) {
+            const size_t c = std::max(m, cap + cap / 2);
+            uint8_t *q = (uint8_t *)realloc(p, c);
+            if (!q) return false;
+            p = q;
+            cap = c;
+        }
+        n = m;
+        return true;
+    }
+    void erase_front(size_t k) {
+        if (k) memmove(p, p + k, n - k);
+        n -= k;
+    }
+    void clear() { n = 0; }
+    void adopt(uint8_t *q, size_t m, size_t c) {
+        free(p);
+        p = q;
+        n = m;
+        cap = c;
+    }
+};
+
 struct BgzfReader {
     FILE *f = nullptr;
     int threads = 1;
     std::vector<uint8_t> comp;     // compressed bytes not yet consumed
     bool eof = false;
     std::string err;
+    // device inflate: a batch of ~DCHUNK compressed bytes per call of fn, the next batch read
+    // and inflated by a helper thread while the caller parses the current one
+    svth_inflate_fn fn = nullptr;
+    void *user = nullptr;
+    static constexpr size_t DCHUNK = 1ull << 30;
+    static constexpr size_t HEAD = 64ull << 20;   // room in front of a batch for the previous one's tail
+    struct Batch {
+        uint8_t *p = nullptr;   // malloc'ed: HEAD bytes, then n inflated bytes
+        size_t n = 0;
+        bool ok = false;
+        std::string err;
+    };
+    std::future<Batch> pending;
+
+    ~BgzfReader() { drop_pending(); }
+    void drop_pending() {
+        if (pending.valid()) free(pending.get().p);
+    }
 
     // Continue at compressed file offset `coff` (a BGZF block start).
     bool seek(uint64_t coff) {
+        drop_pending();
         comp.clear();
         eof = false;
         if (fseeko(f, (off_t)coff, SEEK_SET) != 0) { err = "cannot seek in BAM (BAI offset past the end?)"; return false; }
         return true;
     }
 
-    // Append the next batch of inflated blocks to `out`; false at end of file / on error.
-    bool next(std::vector<uint8_t> &out) {
+    // Read and inflate the next batch through fn (helper thread); ok && n == 0 at end of file.
+    Batch produce() {
+        Batch b;
+        std::vector<svt_bgzf_block> blks;
+        size_t p = 0, u = 0;
+        for (;;) {
+            if (!eof) {
+                const size_t old = comp.size();
+                comp.resize(old + DCHUNK);
+                const size_t got = fread(comp.data() + old, 1, DCHUNK, f);
+                comp.resize(old + got);
+                if (got < DCHUNK) eof = true;
+            }
+            while (p + 18 <= comp.size()) {
+                const uint8_t *h = comp.data() + p;
+                if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { b.err = "not a BGZF file (bad gzip header)"; return b; }
+                const uint16_t xlen = rd16(h + 10);
+                if (p + 12 + xlen > comp.size()) break;
+                size_t bsize = 0;
+                for (size_t x = 0; x + 4 <= xlen;) {
+                    const uint8_t *sf = h + 12 + x;
+                    const uint16_t slen = rd16(sf + 2);
+                    if (sf[0] == 66 && sf[1] == 67 && slen == 2) bsize = (size_t)rd16(sf + 4) + 1;
+                    x += 4 + slen;
+                }
+                if (!bsize || bsize < (size_t)xlen + 20) { b.err = "BGZF block without BC subfield"; return b; }
+                if (p + bsize > comp.size()) break;
+                svt_bgzf_block k;
+                k.coff = p + 12 + xlen;
+                k.clen = (uint32_t)(bsize - xlen - 20);
+                k.uoff = u;
+                k.ulen = rd32(comp.data() + p + bsize - 4);
+                blks.push_back(k);
+                u += k.ulen;
+                p += bsize;
+            }
+            if (!blks.empty() || eof) break;   // (else a single block larger than what was read so far)
+        }
+        if (blks.empty()) {
+            if (!comp.empty()) { b.err = "truncated BGZF block at end of file"; return b; }
+            b.ok = true;
+            return b;
+        }
+        b.p = (uint8_t *)malloc(HEAD + u + 16);
+        if (!b.p) { b.err = "out of host memory"; return b; }
+        char e[256] = {0};
+        if (fn(user, comp.data(), p, blks.data(), blks.size(), b.p + HEAD, u, e, sizeof e) != 0) {
+            free(b.p);
+            b.p = nullptr;
+            b.err = e[0] ? e : "BGZF inflate failed";
+            return b;
+        }
+        comp.erase(comp.begin(), comp.begin() + (ptrdiff_t)p);
+        b.n = u;
+        b.ok = true;
+        return b;
+    }
+
+    // Device path of next(): the pending batch (or a synchronous first one) becomes the buffer,
+    // the unconsumed tail [at, size) moved in front of it; the batch after it starts.
+    bool next_device(Bytes &out, size_t &at) {
+        Batch b = pending.valid() ? pending.get() : produce();
+        if (!b.ok) { err = b.err; return false; }
+        if (b.n == 0) { free(b.p); return false; }   // end of file
+        pending = std::async(std::launch::async, [this] { return produce(); });
+        const size_t tail = out.size() - at;
+        if (tail <= HEAD) {
+            memcpy(b.p + HEAD - tail, out.data() + at, tail);
+            out.adopt(b.p, HEAD + b.n, HEAD + b.n + 16);
+            at = HEAD - tail;
+        } else {   // (a record longer than HEAD: append)
+            out.erase_front(at);
+            at = 0;
+            const size_t base = out.size();
+            if (!out.resize(base + b.n)) { free(b.p); err = "out of host memory"; return false; }
+            memcpy(out.data() + base, b.p + HEAD, b.n);
+            free(b.p);
+        }
+        return true;
+    }
+
+    // Make more inflated bytes available in out (consumed up to `at`); false at end of file /
+    // on error.
+    bool next(Bytes &out, size_t &at) {
+        if (fn) return next_device(out, at);
+        if (at) {
+            out.erase_front(at);
+            at = 0;
+        }
         const size_t CHUNK = 64u << 20;
         for (;;) {
             if (!eof) {
@@ -126,7 +269,7 @@ struct BgzfReader {
             std::vector<size_t> uoff(blks.size() + 1, 0);
             for (size_t i = 0; i < blks.size(); i++) uoff[i + 1] = uoff[i] + blks[i].ulen;
             const size_t base = out.size();
-            out.resize(base + uoff.back());
+            if (!out.resize(base + uoff.back())) { err = "out of host memory"; return false; }
             std::atomic<int> bad{0};
             const Inflater &inf = inflater();
             parallel_for(threads, blks.size() * 4096, [&](size_t b0, size_t b1) {
@@ -357,6 +500,11 @@ svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap)
 
 svth_bam *svth_bam_read_region(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
                                char *err, size_t errcap) {
+    return svth_bam_read_ex(path, threads, tid0, beg0, tid1, end1, nullptr, nullptr, err, errcap);
+}
+
+svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
+                           svth_inflate_fn fn, void *user, char *err, size_t errcap) {
     const bool region = tid0 >= 0;
     auto fail = [&](const std::string &m) -> svth_bam * {
         if (err && errcap) snprintf(err, errcap, "%s", m.c_str());
@@ -367,17 +515,22 @@ svth_bam *svth_bam_read_region(const char *path, int threads, int32_t tid0, int6
     BgzfReader rd;
     rd.f = f;
     rd.threads = threads < 1 ? 1 : threads;
-    std::vector<uint8_t> buf;
+    rd.fn = fn;
+    rd.user = user;
+    Bytes buf;
     size_t at = 0;
     auto need = [&](size_t k) -> bool {
-        while (buf.size() - at < k) {
-            if (at) { buf.erase(buf.begin(), buf.begin() + (ptrdiff_t)at); at = 0; }
-            if (!rd.next(buf)) return false;
-        }
+        while (buf.size() - at < k)
+            if (!rd.next(buf, at)) return false;
         return true;
     };
     svth_bam *b = new svth_bam();
-    auto bail = [&](const std::string &m) { fclose(f); delete b; return fail(rd.err.empty() ? m : rd.err); };
+    auto bail = [&](const std::string &m) {
+        rd.drop_pending();   // (the helper thread reads f)
+        fclose(f);
+        delete b;
+        return fail(rd.err.empty() ? m : rd.err);
+    };
     // header
     if (!need(8) || memcmp(buf.data() + at, "BAM\1", 4) != 0) return bail("not a BAM file");
     const uint32_t l_text = rd32(buf.data() + at + 4);
@@ -493,6 +646,7 @@ svth_bam *svth_bam_read_region(const char *path, int threads, int32_t tid0, int6
         narena += off[nr];
         at = p;
     }
+    rd.drop_pending();
     fclose(f);
     if (!rd.err.empty()) { delete b; return fail(rd.err); }
     const size_t n = b->pos.size();

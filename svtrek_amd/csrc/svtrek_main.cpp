@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <string>
 #include <thread>
 #include <vector>
@@ -56,11 +57,12 @@ void audt_usage() {
     printf("    --devices <i,j,...>               Explicit GPU per shard (overrides --gpus/--device)\n");
     printf("    --batch <num>                     Records per GPU launch [Default: 1048576]\n");
     printf("    --spill-bytes <num>               Initial candidate spill pool per GPU; grown on demand [Default: 67108864]\n");
+    printf("    --inflate <gpu|cpu>               BGZF decompression of the BAM: first GPU or -t host threads [Default: gpu]\n");
 }
 
 struct Args {
     const char *bam = nullptr, *vcf = nullptr, *out = "svtrek.out";
-    int threads = THREADS, verbose = 0, gpus = 1, device = 0;
+    int threads = THREADS, verbose = 0, gpus = 1, device = 0, gpu_inflate = 1;
     size_t batch = 1u << 20;
     std::vector<int> devices;   // device of shard g
     svt_params prm{WIDER, MEDIAN, NARROW, CI_RANGE, CI, MIN_COUNT, 0};
@@ -95,7 +97,8 @@ Args parse_audt(int argc, char **argv) {
         {"consensus-min-count", required_argument, nullptr, 10}, {"help", no_argument, nullptr, 11},
         {"gpus", required_argument, nullptr, 20}, {"device", required_argument, nullptr, 21},
         {"batch", required_argument, nullptr, 22}, {"devices", required_argument, nullptr, 23},
-        {"spill-bytes", required_argument, nullptr, 24}, {nullptr, 0, nullptr, 0}};
+        {"spill-bytes", required_argument, nullptr, 24}, {"inflate", required_argument, nullptr, 25},
+        {nullptr, 0, nullptr, 0}};
     int opt, li;
     while ((opt = getopt_long(argc, argv, "b:v:o:t:h", opts, &li)) != -1) {
         switch (opt) {
@@ -115,6 +118,10 @@ Args parse_audt(int argc, char **argv) {
         case 21: a.device = atoi(optarg); break;
         case 22: a.batch = (size_t)strtoull(optarg, nullptr, 10); break;
         case 24: a.prm.spill_bytes = (uint64_t)strtoull(optarg, nullptr, 10); break;
+        case 25:
+            if (strcmp(optarg, "gpu") && strcmp(optarg, "cpu")) { fprintf(stderr, "[ERROR] --inflate expects gpu or cpu\n"); exit(EXIT_FAILURE); }
+            a.gpu_inflate = strcmp(optarg, "gpu") == 0;
+            break;
         case 23: {
             a.devices.clear();
             for (const char *p = optarg; *p;) {
@@ -226,6 +233,29 @@ void build_shard(const svt_pileup_view &full, const std::vector<svt_locus> &loci
     sh.view.clip = full.clip ? sh.clip.data() : nullptr;
 }
 
+// The ingest's BGZF inflater on the first device (svt_bgzf_inflate), once its context is open.
+struct DeviceInflate {
+    std::shared_future<void> ready;
+    svt_ctx **ctx;
+    const int *open_rc;
+    double ms = 0;   // device time of the inflate kernels
+};
+int device_inflate(void *user, const uint8_t *comp, size_t cb, const svt_bgzf_block *blocks, size_t n, uint8_t *out,
+                   size_t ob, char *err, size_t ecap) {
+    DeviceInflate *d = (DeviceInflate *)user;
+    d->ready.wait();
+    if (*d->open_rc || !*d->ctx) {
+        snprintf(err, ecap, "BGZF inflate: svt_open failed (HIP device?)");
+        return 1;
+    }
+    if (svt_bgzf_inflate(*d->ctx, comp, cb, blocks, n, out, ob) != SVT_OK) {
+        snprintf(err, ecap, "BGZF inflate on the device: %s", svt_last_error(*d->ctx));
+        return 1;
+    }
+    d->ms += svt_bgzf_last_inflate_ms(*d->ctx);
+    return 0;
+}
+
 int audit(int argc, char **argv) {
     Args a = parse_audt(argc, argv);
     const double t0 = now_s();
@@ -236,8 +266,13 @@ int audit(int argc, char **argv) {
     const int G = a.gpus;
     std::vector<svt_ctx *> ctxs(G, nullptr);
     std::vector<int> open_rc(G, 0);
+    std::promise<void> first_open;
+    DeviceInflate dinf{first_open.get_future().share(), &ctxs[0], &open_rc[0]};
     std::thread ot([&] {
-        for (int g = 0; g < G; g++) open_rc[g] = svt_open(&a.prm, a.devices[g], &ctxs[g]);
+        for (int g = 0; g < G; g++) {
+            open_rc[g] = svt_open(&a.prm, a.devices[g], &ctxs[g]);
+            if (g == 0) first_open.set_value();   // the ingest's inflater may start
+        }
     });
     auto close_all = [&] {
         for (svt_ctx *c : ctxs)
@@ -254,7 +289,8 @@ int audit(int argc, char **argv) {
         t_parse_end = now_s();
     });
     char err[512];
-    svth_bam *bam = svth_bam_read(a.bam, a.threads, err, sizeof err);
+    svth_bam *bam = svth_bam_read_ex(a.bam, a.threads, -1, 0, -1, 0, a.gpu_inflate ? device_inflate : nullptr, &dinf,
+                                     err, sizeof err);
     const double t_ingest = now_s();
     vt.join();
     ot.join();
@@ -336,9 +372,11 @@ int audit(int argc, char **argv) {
     svth_free(out);
     printf("[INFO] Ended processing variation file\n");
     if (a.verbose)   // --verbose is parsed but unused by the reference; here: stage timings on stderr
-        fprintf(stderr, "[svtrek_amd] ingest %.3fs  vcf-read+parse %.3fs (beside the ingest)  load+refine %.3fs "
-                        "(load %.3fs)  print %.3fs  records %zu\n",
-                t_ingest - t0, t_parse_end - t0, t_refine - t_parse, *std::max_element(load_s.begin(), load_s.end()),
+        fprintf(stderr, "[svtrek_amd] ingest %.3fs (inflate %s%s)  vcf-read+parse %.3fs (beside the ingest)  "
+                        "load+refine %.3fs (load %.3fs)  print %.3fs  records %zu\n",
+                t_ingest - t0, a.gpu_inflate ? "gpu, kernels " : "cpu",
+                a.gpu_inflate ? (std::to_string(dinf.ms / 1e3).substr(0, 5) + "s").c_str() : "",
+                t_parse_end - t0, t_refine - t_parse, *std::max_element(load_s.begin(), load_s.end()),
                 now_s() - t_refine, loci.size());
     return 0;
 }

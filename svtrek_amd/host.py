@@ -25,6 +25,9 @@ def load_host() -> C.CDLL:
         L.svth_bam_read_region.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int64, C.c_int32, C.c_int64,
                                            C.c_char_p, C.c_size_t]
         L.svth_bam_read_region.restype = P
+        L.svth_bam_read_ex.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int64, C.c_int32, C.c_int64, P, P,
+                                       C.c_char_p, C.c_size_t]
+        L.svth_bam_read_ex.restype = P
         L.svth_vcf_parse.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
         L.svth_vcf_parse.restype = P
         L.svth_vcf_count.argtypes = [P]
@@ -61,17 +64,33 @@ def load_host() -> C.CDLL:
     return _host
 
 
-def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | None = None) -> tuple[Pileup, dict]:
+INFLATE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                         C.c_void_p, C.c_size_t)
+
+
+def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | None = None,
+             inflate=None) -> tuple[Pileup, dict]:
     """The BAM as a columnar pileup.  region = (tid0, beg0, tid1, end1): only the records from
     the BAI's linear-index offset of (tid0, beg0) up to the first at or past (tid1, end1)
-    (svth_bam_read_region; needs `path`.bai) -- what one shard's queries can yield."""
+    (svth_bam_read_region; needs `path`.bai) -- what one shard's queries can yield.
+    inflate = an Engine: the BGZF blocks are inflated by its svt_bgzf_inflate (the device, in
+    ~1 GiB batches overlapped with the record parse) instead of host threads."""
     L = load_host()
     err = C.create_string_buffer(512)
-    if region is None:
-        h = L.svth_bam_read(path.encode(), threads, err, 512)
-    else:
-        t0, b0, t1, e1 = (int(x) for x in region)
+    t0, b0, t1, e1 = (int(x) for x in region) if region is not None else (-1, 0, -1, 0)
+    if inflate is None:
         h = L.svth_bam_read_region(path.encode(), threads, t0, b0, t1, e1, err, 512)
+    else:
+        lib, ctx = inflate.lib, inflate._h
+
+        def cb(_user, comp, cbytes, blocks, n, out, obytes, e, ecap):
+            rc = lib.svt_bgzf_inflate(ctx, comp, cbytes, blocks, n, out, obytes)
+            if rc:
+                m = lib.svt_last_error(ctx)[:max(int(ecap) - 1, 0)]
+                C.memmove(e, m + b"\0", len(m) + 1)
+            return rc
+        fn = INFLATE_FN(cb)
+        h = L.svth_bam_read_ex(path.encode(), threads, t0, b0, t1, e1, C.cast(fn, C.c_void_p), None, err, 512)
     if not h:
         raise OSError(err.value.decode())
     try:

@@ -274,3 +274,28 @@ def test_vcf_batch_parse_and_format(threads):
     res["end"] = np.where(rng2.random(len(loci)) < 0.3, 0xFFFFFFFF, rng2.integers(0, 2**32, len(loci)))
     assert host.format_batch(loci, res, threads=threads) == "".join(
         host.format_result(loci[k], res[k]) for k in range(len(loci)))
+
+
+@pytest.mark.parametrize("region", [None, "mid"])
+def test_bam_read_with_inflate_callback(tmp_path, region):
+    """svth_bam_read_ex with an inflater callback (the CLI's device path; here the CPU backend's
+    svt_bgzf_inflate behind the same ABI) reads the same pileup as the host-thread inflate, for
+    the whole file and for a BAI region."""
+    import ctypes
+
+    from svtrek_amd import Engine, Params
+    from svtrek_amd._lib import bind_abi
+    cfg = sim.SimConfig(seed=21, n_targets=3, n_loci=60, del_frac=0.5, coverage=8, p_clip_ends=0.3)
+    r = sim.generate(cfg, keep_handle=True)
+    path = str(tmp_path / "x.bam")
+    sim.write_bam(r, path, with_seq=True, level=1)
+    reg = None if region is None else (1, 20000, 2, 10 ** 9)
+    want, wi = host.read_bam(path, threads=3, region=reg)
+    cpu = Engine(Params(), device=0, lib=bind_abi(ctypes.CDLL(os.path.join(ROOT, "oracle", "libsvtrek_cpu.so"))))
+    try:
+        got, gi = host.read_bam(path, threads=3, region=reg, inflate=cpu)
+    finally:
+        cpu.close()
+    assert wi == gi
+    for k in ("tid_off", "pos", "endpos", "cig_off", "cigar", "clip"):
+        assert np.array_equal(getattr(want, k), getattr(got, k)), k

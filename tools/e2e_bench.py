@@ -29,6 +29,7 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--level", type=int, default=1, help="BGZF deflate level for the written BAM")
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--inflate", default="gpu,cpu", help="BGZF inflate modes to time (CLI --inflate), comma-separated")
     ap.add_argument("--region-sample", type=int, default=0, metavar="K",
                     help="the CPU baseline's sample instead of the whole workload: the first K loci of contig 1 "
                          "(genomic order) and the BAM of their region, with SEQ/QUAL -- the same bytes bench.py's "
@@ -55,26 +56,32 @@ def main() -> int:
     sim.write_vcf(loci, vcf)
     prep = time.perf_counter() - t
     cli = os.path.join(ROOT, "svtrek_amd", "svtrek")
-    times = []
-    for _ in range(a.reps):
-        t = time.perf_counter()
-        p = subprocess.run([cli, "audt", "-b", bam, "-v", vcf, "-t", str(a.t), "--verbose"], stdout=subprocess.PIPE,
-                           stderr=subprocess.PIPE, timeout=1800)
-        times.append(time.perf_counter() - t)
-        if p.returncode != 0:
-            print(p.stderr.decode()[-2000:], file=sys.stderr)
-            return p.returncode
-    lines = p.stdout.count(b"\n") - 2
-    stages = [l for l in p.stderr.decode(errors="replace").splitlines() if l.startswith("[svtrek_amd]")]
-    best = min(times)
-    print(json.dumps({
-        "metric": "end-to-end svtrek audt (BAM ingest + H2D + refine + print)", "workload": a.workload,
-        "loci": int(len(loci)), "printed_records": int(lines), "bam_bytes": os.path.getsize(bam),
-        "with_seq": a.with_seq or bool(a.region_sample), "inflate_threads": a.t, "seconds_best": round(best, 3),
-        "seconds_all": [round(x, 3) for x in times], "loci_per_s": round(len(loci) / best, 1),
-        "region_sample": {"loci": a.region_sample, "region": region} if a.region_sample else None,
-        "disk_free_gb_before": round(free_gb, 1),
-        "prep_seconds": round(prep, 1), "stages_last_run": stages[-1] if stages else None}))
+    outs = {}
+    for mode in a.inflate.split(","):
+        times = []
+        for _ in range(a.reps):
+            t = time.perf_counter()
+            p = subprocess.run([cli, "audt", "-b", bam, "-v", vcf, "-t", str(a.t), "--verbose", "--inflate", mode],
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=1800)
+            times.append(time.perf_counter() - t)
+            if p.returncode != 0:
+                print(p.stderr.decode()[-2000:], file=sys.stderr)
+                return p.returncode
+        outs[mode] = p.stdout
+        lines = p.stdout.count(b"\n") - 2
+        stages = [l for l in p.stderr.decode(errors="replace").splitlines() if l.startswith("[svtrek_amd]")]
+        best = min(times)
+        print(json.dumps({
+            "metric": "end-to-end svtrek audt (BAM ingest + H2D + refine + print)", "workload": a.workload,
+            "inflate": mode, "loci": int(len(loci)), "printed_records": int(lines), "bam_bytes": os.path.getsize(bam),
+            "with_seq": a.with_seq or bool(a.region_sample), "host_threads": a.t, "seconds_best": round(best, 3),
+            "seconds_all": [round(x, 3) for x in times], "loci_per_s": round(len(loci) / best, 1),
+            "region_sample": {"loci": a.region_sample, "region": region} if a.region_sample else None,
+            "disk_free_gb_before": round(free_gb, 1),
+            "prep_seconds": round(prep, 1), "stages_last_run": stages[-1] if stages else None}), flush=True)
+    if len(outs) > 1 and len(set(outs.values())) != 1:
+        print("stdout differs between inflate modes", file=sys.stderr)
+        return 1
     return 0
 
 
