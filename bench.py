@@ -11,9 +11,11 @@ refines the g-th contiguous slice against only the reads its queries can reach
 ("scaling": "strong").
 
 A step is the whole per-locus path from the resident columnar pileup to refined calls:
-  1. the device index build (svt_reindex: ix_census_kernel -- a streaming reduction of every
-     range's totals --, a hipcub scan of them, then index_kernel<emit> -- every read's CIGAR
-     walked once, refinement.c:118-159/:184-221/:295-318),
+  1. the device index build (svt_reindex: every read's CIGAR walked once,
+     refinement.c:118-159/:184-221/:295-318): for short reads (cfg4) ix2_census_kernel +
+     ix2_emit_kernel, one lane per read; for long reads ix_census_kernel (a streaming
+     reduction) + index_kernel<emit> (the stream walk); a hipcub scan of the census totals
+     between the two),
   2. one batched refine launch over the rank's slice (svt_refine_device_records:
      refine_lane_kernel + refine_redo_kernel; loci and 16-B result records resident in HBM),
   3. at N > 1, the one collective of the path: an RCCL gather to rank 0 of the slice's 16-B
@@ -126,6 +128,7 @@ def _engine_version() -> str:
 
 
 STEP_KERNELS = ("ix2_census_kernel", "ix2_emit_kernel", "refine_lane_kernel", "refine_redo_kernel")
+STREAM_INDEX_KERNELS = ("ix_census_kernel", "index_kernel<emit>")   # the long-read index build (svt_index.inc)
 
 
 def _traffic(workload: str, kernel: str, records: bool) -> tuple[int | None, str | None]:
@@ -343,7 +346,8 @@ def main() -> int:
                          "traffic_over_alg": round(traffic / ref_bytes, 4) if traffic else None,
                          "traffic_gbs": round(traffic / (step_ms * 1e-3) / 1e9, 2) if traffic else None,
                          "traffic_source": traffic_src,
-                         "kernel": "step = index build (" + ", ".join(STEP_KERNELS[:2]) + ") + refine (" +
+                         "kernel": "step = index build (" + ", ".join(STEP_KERNELS[:2] if load_stats.get("index_kind") == 1
+                                                                      else STREAM_INDEX_KERNELS) + ") + refine (" +
                                    (refine_kernel + (", refine_redo_kernel" if refine_kernel == "refine_lane_kernel"
                                                      else "")) + ")",
                          "step_ms_mean": round(step_ms, 5),
@@ -357,9 +361,9 @@ def main() -> int:
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), per read 24 + 8 B "
-                                                "(census: soff, rec; cnt written) and 32 + 32 B (emit: cnt, soff, rec; "
-                                                "offsets written), 16 B/span event, 16 B/lead chunk unit (svt_load_stats.index_bytes)",
+                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), per read 96 B (lane per "
+                                                "read: census soff, rec, counts; emit counts, soff, rec, offsets) or 72 B "
+                                                "(stream walk), 16 B/span event, 16 B/lead chunk unit (svt_load_stats.index_bytes)",
                          },
                          "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
                                           "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),

@@ -278,6 +278,7 @@ typedef struct svt_load_stats {
     uint64_t span_events;   /* D-list + I-list span events of the pileup                         */
     uint64_t lead_blocks;   /* 16-B lead chunk units (leading-S reads: header + 4 words / 32 ops) */
     uint64_t slow_reads;    /* reads whose walk reaches 2^28 bases or position 2^29              */
+    uint64_t index_kind;    /* the index build used: 1 lane per read, 2 stream walk              */
 } svt_load_stats;
 svt_status svt_last_load_stats(const svt_ctx *ctx, svt_load_stats *out);
 

@@ -98,6 +98,7 @@ class SvtLoadStats(C.Structure):
         ("span_events", C.c_uint64),
         ("lead_blocks", C.c_uint64),
         ("slow_reads", C.c_uint64),
+        ("index_kind", C.c_uint64),
     ]
 
 

@@ -2007,7 +2007,8 @@ struct svt_ctx {
     uint32_t *d_xlist = nullptr;      // [n_ranges] ranges for the exact census
     uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
     uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
-    bool ix_lane = true;              // index build: lane per read (svt_index2.inc) / stream walk (SVTREK_IX=stream)
+    int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
+                                      // walk (svt_index.inc) -- SVTREK_IX=auto|lane|stream
     uint64_t *d_tot = nullptr;
     void *d_scan_tmp = nullptr;       // hipcub scan scratch
     size_t scan_tmp_bytes = 0;
@@ -2392,7 +2393,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     const char *g = getenv("SVTREK_GATHER");   // "span1": the one-wave-per-window kernel at every batch size
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *x = getenv("SVTREK_IX_EXACT")) c->ix_exact = atoi(x) == 1;
-    if (const char *x = getenv("SVTREK_IX")) c->ix_lane = strcmp(x, "stream") != 0;
+    if (const char *x = getenv("SVTREK_IX")) c->ix_mode = strcmp(x, "lane") == 0 ? 1 : strcmp(x, "stream") == 0 ? 2 : 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
@@ -2502,8 +2503,12 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
             if (e) (void)hipEventDestroy(e);
         return r;
     };
-    // lane per read (svt_index2.inc) unless a 64-read group is too large for its 32-bit offsets
-    const bool lane = c->ix_lane && c->n_groups > 0;
+    // lane per read (svt_index2.inc) for short reads -- a wave's 64 reads then take a few steps
+    // each; long reads (a lane walking thousands of ops waits on its loads) take the stream walk,
+    // which spreads every slot of 256 ops over the wave (cfg4 28 ops/read: lane 1.15 vs stream
+    // 1.24 ms; cfg5 1715 ops/read: lane 31.1 vs stream 18.7 ms); never for a group of > 2^27 ops
+    const bool lane = c->n_groups > 0 && (c->ix_mode == 1 || (c->ix_mode == 0 && c->n_ops <= 64ull * c->n_reads));
+    c->load_stats.index_kind = lane ? 1u : 2u;
     const uint32_t nparts = lane ? c->n_groups : c->n_ranges;   // what the scan runs over
     Ix2Args a2{a, c->d_cnt, (uint64_t)c->n_reads, c->n_groups};
     const dim3 grid2((unsigned)((c->n_groups + IX2_WPB - 1) / IX2_WPB)), block2(64 * IX2_WPB);
@@ -2730,10 +2735,12 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         c->load_stats.span_events = c->n_evD + c->n_evI;
         c->load_stats.lead_blocks = c->n_lead_blocks;
         c->load_stats.slow_reads = c->n_slow;
-        // (lane-per-read index) census: stream + soff + rec (24 B/read), cnt written (8 B/read);
-        // emit: cnt + soff + rec (32 B/read) + stream, the per-read offsets (32 B/read), events
-        // and lead units written
-        c->load_stats.index_bytes = 8ull * nstream + 32ull * R + 32ull * R + 32ull * R +
+        // lane per read: census stream + soff + rec (24 B/read), cnt written (8 B/read); emit cnt
+        // + soff + rec (32 B/read) + stream, the per-read offsets (32 B/read) written.  Stream
+        // walk: census stream + rec (16 B/read); emit stream + soff + rec (24 B/read), offsets.
+        // Both: the events and lead units written.
+        const uint64_t per_read = c->load_stats.index_kind == 1 ? 96u : 72u;
+        c->load_stats.index_bytes = 8ull * nstream + per_read * R +
                                     16ull * (c->n_evD + c->n_evI) + 16ull * c->n_lead_blocks;
     } else {
         for (auto *pp : {&c->d_spD, &c->d_spI})
