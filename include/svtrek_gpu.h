@@ -302,8 +302,8 @@ typedef struct svt_bgzf_block {
  * data does not inflate to exactly ulen bytes. */
 svt_status svt_bgzf_inflate(svt_ctx *ctx, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
                             size_t n, uint8_t *out, size_t out_bytes);
-/* The same on device buffers (the block table on the device too; d_comp readable up to 3
- * bytes past every block's data), asynchronous on hip_stream; svt_bgzf_inflate_status waits
+/* The same on device buffers (the block table on the device too; d_comp 16-B aligned and
+ * readable up to 48 bytes past every block's data), asynchronous on hip_stream; svt_bgzf_inflate_status waits
  * for the stream and reports the first corrupt block (0xffffffff: none). */
 svt_status svt_bgzf_inflate_device(svt_ctx *ctx, const uint8_t *d_comp, const svt_bgzf_block *d_blocks, size_t n,
                                    uint8_t *d_out, void *hip_stream);

@@ -1967,8 +1967,8 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *comp, const 
     const InfFast F(tabs + ln, WAVE);
     for (uint32_t b = g; b < n; b += gridDim.x * WAVE) {
         const svt_bgzf_block k = blk[b];
-        const uint64_t a = k.coff & ~3ull;
-        const int rc = inf_block(reinterpret_cast<const uint32_t *>(comp + a), (uint32_t)(k.coff - a), k.clen,
+        const uint64_t a = k.coff & ~15ull;
+        const int rc = inf_block(reinterpret_cast<const InfV4 *>(comp + a), (uint32_t)(k.coff - a), k.clen,
                                  out + k.uoff, k.ulen, F, scratch[g]);
         if (rc != INF_OK) atomicMin(err, b);
     }
@@ -3116,7 +3116,7 @@ svt_status svt_bgzf_inflate(svt_ctx *c, const uint8_t *comp, size_t comp_bytes, 
         cap = bytes;
         return SVT_OK;
     };
-    if ((s = grow(c->d_infc, c->infc_cap, comp_bytes + 16)) || (s = grow(c->d_info, c->info_cap, std::max<size_t>(out_bytes, 1))) ||
+    if ((s = grow(c->d_infc, c->infc_cap, comp_bytes + 64)) || (s = grow(c->d_info, c->info_cap, std::max<size_t>(out_bytes, 1))) ||
         (s = grow(c->d_infb, c->infb_cap, n * sizeof(svt_bgzf_block))))
         return s;
     HIP_TRY(c, hipMemcpy(c->d_infc, comp, comp_bytes, hipMemcpyHostToDevice));

@@ -52,44 +52,62 @@ struct InfSlow {               // per block, scratch
 
 enum : int { INF_OK = 0, INF_EDATA = 1, INF_EOUT = 2, INF_EIN = 3 };
 
-// The bit reader takes the stream as aligned 32-bit words: the block's data starts `skip` bytes
-// into word 0, and words past the last one holding data read as zeros (a valid stream never
-// consumes them; past() tells a stream that did).  fill() leaves >= 33 bits buffered, which
+// The bit reader takes the stream as 16-B aligned vectors: the block's data starts `skip` bytes
+// (< 16) into vector 0, and vectors past the last one holding data read as zeros (a valid stream
+// never consumes them; past() tells a stream that did).  Two vectors beyond the one being
+// consumed are always in flight (a lane's next loads are issued ~ 32 bytes before their bits
+// are needed, so the decode does not wait on them).  fill() leaves >= 33 bits buffered, which
 // covers every step between two fills (a code of <= 15 bits + <= 13 extra bits).
+struct InfV4 {
+    uint32_t x, y, z, w;
+};
 struct InfBits {
-    const uint32_t *w;
-    uint32_t nw, q;    // words holding data, next word
-    uint32_t skip, n;  // data start in word 0 (bytes), data length (bytes)
-    uint64_t bb;       // bit buffer (LSB = next bit)
-    int nb;            // valid bits in bb
+    const InfV4 *v;
+    uint32_t nv, vi, wi;  // vectors holding data, index of `cur`, next word of `cur`
+    InfV4 cur, n1, n2;    // the vector being consumed, the next two
+    uint32_t skip, n;     // data start in vector 0 (bytes), data length (bytes)
+    uint64_t bb;          // bit buffer (LSB = next bit)
+    int nb;               // valid bits in bb
 
-    SVT_HD void init(const uint32_t *words, uint32_t skip_bytes, uint32_t len) {
-        w = words;
+    SVT_HD InfV4 ld(uint32_t i) const { return i < nv ? v[i] : InfV4{0u, 0u, 0u, 0u}; }
+    SVT_HD void init(const InfV4 *vecs, uint32_t skip_bytes, uint32_t len) {
+        v = vecs;
         skip = skip_bytes;
         n = len;
-        nw = (skip_bytes + len + 3u) >> 2;
-        q = 0;
+        nv = (skip_bytes + len + 15u) >> 4;
+        cur = ld(0);
+        n1 = ld(1);
+        n2 = ld(2);
+        vi = 0;
+        wi = skip_bytes >> 2;
         bb = 0;
         nb = 0;
         fill();
-        bb >>= 8 * skip;
-        nb -= 8 * (int)skip;
+        drop(8 * (int)(skip_bytes & 3u));
     }
     SVT_HD void fill() {
         while (nb <= 32) {
-            const uint64_t x = q < nw ? w[q] : 0u;
-            q++;
-            bb |= x << nb;
+            const uint32_t x = wi == 0 ? cur.x : wi == 1 ? cur.y : wi == 2 ? cur.z : cur.w;
+            bb |= (uint64_t)x << nb;
             nb += 32;
+            if (++wi == 4) {
+                cur = n1;
+                n1 = n2;
+                vi++;
+                n2 = ld(vi + 2);
+                wi = 0;
+            }
         }
     }
-    SVT_HD bool past() const { return 32ull * q - (uint64_t)nb - 8ull * skip > 8ull * n; }   // consumed more than n bytes
+    SVT_HD bool past() const {   // consumed more than n bytes
+        return 32ull * (4ull * vi + wi) - (uint64_t)nb - 8ull * skip > 8ull * n;
+    }
     SVT_HD uint32_t peek(int k) { return (uint32_t)(bb & ((1ull << k) - 1)); }
     SVT_HD void drop(int k) { bb >>= k; nb -= k; }
     SVT_HD uint32_t get(int k) {   // k <= 32, after fill() guaranteeing k bits
-        const uint32_t v = peek(k);
+        const uint32_t v_ = peek(k);
         drop(k);
-        return v;
+        return v_;
     }
 };
 
@@ -172,10 +190,10 @@ SVT_HD int inf_ord(int i) {
     return (int)((i < 12 ? lo >> (5 * i) : hi >> (5 * (i - 12))) & 31u);
 }
 
-// Inflate one raw DEFLATE stream of clen bytes, starting `skip` bytes into the aligned words
-// `in`, to out[0..ulen).  Returns INF_OK only when the stream ends (BFINAL block done) with
-// exactly ulen bytes written and no read past clen.
-SVT_HD int inf_block(const uint32_t *in, uint32_t skip, uint32_t clen, uint8_t *out, uint32_t ulen, const InfFast &F,
+// Inflate one raw DEFLATE stream of clen bytes, starting `skip` (< 16) bytes into the 16-B
+// aligned `in`, to out[0..ulen).  Returns INF_OK only when the stream ends (BFINAL block done)
+// with exactly ulen bytes written and no read past clen.
+SVT_HD int inf_block(const InfV4 *in, uint32_t skip, uint32_t clen, uint8_t *out, uint32_t ulen, const InfFast &F,
                      InfSlow &S) {
     InfBits br;
     br.init(in, skip, clen);
@@ -260,7 +278,16 @@ SVT_HD int inf_block(const uint32_t *in, uint32_t skip, uint32_t clen, uint8_t *
                 const uint32_t dist = inf_dbase(d) + br.get(inf_dext(d));
                 if (dist > op) return INF_EDATA;
                 if (op + len > ulen) return INF_EOUT;
-                for (uint32_t k = 0; k < len; k++, op++) out[op] = out[op - dist];
+                uint32_t k = 0;
+                if (dist >= 8)   // 8 bytes a step: the loads of a step issued before its stores
+                    for (; k + 8 <= len; k += 8, op += 8) {
+                        uint8_t t[8];
+#pragma unroll
+                        for (int i = 0; i < 8; i++) t[i] = out[op - dist + i];
+#pragma unroll
+                        for (int i = 0; i < 8; i++) out[op + i] = t[i];
+                    }
+                for (; k < len; k++, op++) out[op] = out[op - dist];
             }
         } else {
             return INF_EDATA;

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.fixture(scope="module")
 def shim(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("inf") / "shim.so")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-Werror",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-Werror", "-Wno-unknown-pragmas",
                     "-I", os.path.join(ROOT, "svtrek_amd", "csrc"), "-o", out,
                     os.path.join(ROOT, "tests", "native", "inflate_shim.cpp")], check=True)
     return ctypes.CDLL(out)
@@ -53,7 +53,7 @@ def test_inflate_matches_zlib(shim, kind):
         for strat in (zlib.Z_DEFAULT_STRATEGY, zlib.Z_FIXED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE):
             c = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strat)
             comp = c.compress(d) + c.flush()
-            for skip in range(4):
+            for skip in (0, 3, 5, 15):
                 rc, got = _inf(shim, comp, len(d), skip)
                 assert rc == 0 and got == d, (level, strat, skip, rc)
 
