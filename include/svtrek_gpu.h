@@ -310,6 +310,10 @@ svt_status svt_bgzf_inflate_device(svt_ctx *ctx, const uint8_t *d_comp, const sv
 svt_status svt_bgzf_inflate_status(svt_ctx *ctx, void *hip_stream, uint32_t *bad_block);
 /* Device time (ms, HIP events) of the last svt_bgzf_inflate's kernel. */
 double svt_bgzf_last_inflate_ms(const svt_ctx *ctx);
+/* Pinned host memory on the context's device (svt_bgzf_inflate copies from / to it at full
+ * PCIe speed); NULL on failure.  Free with svt_host_free. */
+void *svt_host_alloc(svt_ctx *ctx, size_t bytes);
+void  svt_host_free(svt_ctx *ctx, void *p);
 
 const char *svt_last_error(const svt_ctx *ctx);
 void        svt_close(svt_ctx *ctx);

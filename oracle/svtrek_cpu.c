@@ -257,6 +257,8 @@ svt_status svt_bgzf_inflate_status(svt_ctx *c, void *s, uint32_t *bad) {
     return *bad == 0xffffffffu ? SVT_OK : fail(c, SVT_EINVAL, "corrupt BGZF block %u", *bad);
 }
 double svt_bgzf_last_inflate_ms(const svt_ctx *c) { (void)c; return 0.0; }
+void *svt_host_alloc(svt_ctx *c, size_t bytes) { (void)c; return malloc(bytes ? bytes : 1); }
+void svt_host_free(svt_ctx *c, void *p) { (void)c; free(p); }
 
 const char *svt_last_error(const svt_ctx *c) { return c ? c->err : "NULL context"; }
 void svt_close(svt_ctx *c) {

@@ -111,6 +111,7 @@ ENGINE_SYMBOLS = (
     "svt_poa_deferred", "svt_last_load_stats", "svt_open_multi", "svt_device_count",
     "svt_refine_device_records", "svt_reindex",
     "svt_bgzf_inflate", "svt_bgzf_inflate_device", "svt_bgzf_inflate_status", "svt_bgzf_last_inflate_ms",
+    "svt_host_alloc", "svt_host_free",
 )
 
 _engine = None
@@ -181,6 +182,10 @@ def bind_abi(lib: C.CDLL) -> C.CDLL:
     lib.svt_bgzf_inflate_status.argtypes = [P, P, C.POINTER(C.c_uint32)]
     lib.svt_bgzf_last_inflate_ms.argtypes = [P]
     lib.svt_bgzf_last_inflate_ms.restype = C.c_double
+    lib.svt_host_alloc.argtypes = [P, C.c_size_t]
+    lib.svt_host_alloc.restype = P
+    lib.svt_host_free.argtypes = [P, P]
+    lib.svt_host_free.restype = None
     for name in ("svt_bgzf_inflate", "svt_bgzf_inflate_device", "svt_bgzf_inflate_status",
                  "svt_open", "svt_open_multi", "svt_refine_device_records", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
                  "svt_reindex", "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):

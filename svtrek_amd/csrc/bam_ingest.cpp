@@ -15,6 +15,8 @@
 // A coordinate-sorted BAM (the only kind that has a BAI) needs no reordering; other
 // files are stably sorted by (tid, pos) at the end.  SEQ/QUAL/aux are never copied.
 #include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -71,25 +73,29 @@ const Inflater &inflater() {
     return inf;
 }
 
-// Growable byte buffer without value-initialisation; adopt() takes over a malloc'ed block (the
-// device-inflated batches are handed over without a copy).
+// Growable byte buffer without value-initialisation; view() points it at a buffer owned by the
+// reader (the device-inflated batches are handed over without a copy).
 struct Bytes {
     uint8_t *p = nullptr;
     size_t n = 0, cap = 0;
     Bytes() = default;
     Bytes(const Bytes &) = delete;
     Bytes &operator=(const Bytes &) = delete;
-    ~Bytes() { free(p); }
+    ~Bytes() {
+        if (owned) free(p);
+    }
     size_t size() const { return n; }
     uint8_t *data() { return p; }
     const uint8_t *data() const { return p; }
     bool resize(size_t m) {
         if (m > cap) {
             const size_t c = std::max(m, cap + cap / 2);
-            uint8_t *q = (uint8_t *)realloc(p, c);
+            uint8_t *q = (uint8_t *)(owned ? realloc(p, c) : malloc(c));
             if (!q) return false;
+            if (!owned && n) memcpy(q, p, n);
             p = q;
             cap = c;
+            owned = true;
         }
         n = m;
         return true;
@@ -99,11 +105,12 @@ struct Bytes {
         n -= k;
     }
     void clear() { n = 0; }
-    void adopt(uint8_t *q, size_t m, size_t c) {
-        free(p);
+    bool owned = true;   // false: a view of a buffer someone else frees (view())
+    void view(uint8_t *q, size_t m) {
+        if (owned) free(p);
         p = q;
-        n = m;
-        cap = c;
+        n = cap = m;
+        owned = false;
     }
 };
 
@@ -113,52 +120,100 @@ struct BgzfReader {
     std::vector<uint8_t> comp;     // compressed bytes not yet consumed
     bool eof = false;
     std::string err;
-    // device inflate: a batch of ~DCHUNK compressed bytes per call of fn, the next batch read
-    // and inflated by a helper thread while the caller parses the current one
-    svth_inflate_fn fn = nullptr;
-    void *user = nullptr;
-    static constexpr size_t DCHUNK = 1ull << 30;
+    // device inflate (svth_inflater): batches of ~`batch` compressed bytes, read with parallel
+    // preads into a reused input buffer and inflated by inf->inflate into one of two reused
+    // output buffers (from inf->alloc: pinned host memory, so the copies to and from the device
+    // run at full speed); the next batch is read and inflated by a helper thread while the
+    // caller parses the current one
+    const svth_inflater *inf = nullptr;
     static constexpr size_t HEAD = 64ull << 20;   // room in front of a batch for the previous one's tail
+    struct Buf {
+        uint8_t *p = nullptr;
+        size_t cap = 0;
+    };
+    Buf cin, outs[2];     // compressed input; output buffers (one parsed, one being filled)
+    size_t cin_n = 0;     // bytes held in cin (a partial block left from the previous batch first)
+    int fill_i = 0;       // the output buffer the next batch goes to
+    uint64_t foff = 0, fsize = 0;
     struct Batch {
-        uint8_t *p = nullptr;   // malloc'ed: HEAD bytes, then n inflated bytes
+        uint8_t *p = nullptr;   // outs[i].p: HEAD bytes, then n inflated bytes
         size_t n = 0;
         bool ok = false;
         std::string err;
     };
     std::future<Batch> pending;
 
-    ~BgzfReader() { drop_pending(); }
+    ~BgzfReader() {
+        drop_pending();
+        for (Buf *b : {&cin, &outs[0], &outs[1]}) release(*b);
+    }
     void drop_pending() {
-        if (pending.valid()) free(pending.get().p);
+        if (pending.valid()) (void)pending.get();
+    }
+    void release(Buf &b) {
+        if (b.p) {
+            if (inf && inf->release) inf->release(inf->user, b.p);
+            else free(b.p);
+        }
+        b = Buf{};
+    }
+    bool reserve(Buf &b, size_t need, size_t keep) {   // grow to >= need, keeping the first `keep` bytes
+        if (need <= b.cap) return true;
+        const size_t c = std::max(need, b.cap + b.cap / 2);
+        uint8_t *q = inf && inf->alloc ? (uint8_t *)inf->alloc(inf->user, c) : (uint8_t *)malloc(c);
+        if (!q) return false;
+        if (keep) memcpy(q, b.p, keep);
+        release(b);
+        b.p = q;
+        b.cap = c;
+        return true;
     }
 
     // Continue at compressed file offset `coff` (a BGZF block start).
     bool seek(uint64_t coff) {
         drop_pending();
         comp.clear();
+        cin_n = 0;
+        foff = coff;
         eof = false;
         if (fseeko(f, (off_t)coff, SEEK_SET) != 0) { err = "cannot seek in BAM (BAI offset past the end?)"; return false; }
         return true;
     }
 
-    // Read and inflate the next batch through fn (helper thread); ok && n == 0 at end of file.
+    // Read the next batch of compressed bytes after what cin holds, `threads` preads at once.
+    bool read_batch(size_t want) {
+        if (foff >= fsize) { eof = true; return true; }
+        want = (size_t)std::min<uint64_t>(want, fsize - foff);
+        if (!reserve(cin, cin_n + want + 64, cin_n)) return false;
+        const int fd = fileno(f);
+        std::atomic<int> bad{0};
+        parallel_for(threads, want, [&](size_t a, size_t b) {
+            for (size_t o = a; o < b;) {
+                const ssize_t r = pread(fd, cin.p + cin_n + o, b - o, (off_t)(foff + o));
+                if (r <= 0) { bad = 1; return; }
+                o += (size_t)r;
+            }
+        });
+        if (bad) { err = "cannot read BAM"; return false; }
+        cin_n += want;
+        foff += want;
+        if (foff >= fsize) eof = true;
+        return true;
+    }
+
+    // Read and inflate the next batch (helper thread); ok && n == 0 at end of file.
     Batch produce() {
         Batch b;
         std::vector<svt_bgzf_block> blks;
         size_t p = 0, u = 0;
+        const size_t want = inf->batch_bytes ? inf->batch_bytes : (1ull << 30);
         for (;;) {
-            if (!eof) {
-                const size_t old = comp.size();
-                comp.resize(old + DCHUNK);
-                const size_t got = fread(comp.data() + old, 1, DCHUNK, f);
-                comp.resize(old + got);
-                if (got < DCHUNK) eof = true;
-            }
-            while (p + 18 <= comp.size()) {
-                const uint8_t *h = comp.data() + p;
+            if (!eof && !read_batch(want)) { b.err = err; return b; }
+            while (p + 18 <= cin_n) {
+                const uint8_t *h = cin.p + p;
                 if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { b.err = "not a BGZF file (bad gzip header)"; return b; }
                 const uint16_t xlen = rd16(h + 10);
-                if (p + 12 + xlen > comp.size()) break;
+                if (p + 12 + xlen > cin_n) break;
                 size_t bsize = 0;
                 for (size_t x = 0; x + 4 <= xlen;) {
                     const uint8_t *sf = h + 12 + x;
@@ -167,12 +222,12 @@ struct BgzfReader {
                     x += 4 + slen;
                 }
                 if (!bsize || bsize < (size_t)xlen + 20) { b.err = "BGZF block without BC subfield"; return b; }
-                if (p + bsize > comp.size()) break;
+                if (p + bsize > cin_n) break;
                 svt_bgzf_block k;
                 k.coff = p + 12 + xlen;
                 k.clen = (uint32_t)(bsize - xlen - 20);
                 k.uoff = u;
-                k.ulen = rd32(comp.data() + p + bsize - 4);
+                k.ulen = rd32(cin.p + p + bsize - 4);
                 blks.push_back(k);
                 u += k.ulen;
                 p += bsize;
@@ -180,52 +235,46 @@ struct BgzfReader {
             if (!blks.empty() || eof) break;   // (else a single block larger than what was read so far)
         }
         if (blks.empty()) {
-            if (!comp.empty()) { b.err = "truncated BGZF block at end of file"; return b; }
+            if (cin_n) { b.err = "truncated BGZF block at end of file"; return b; }
             b.ok = true;
             return b;
         }
-        b.p = (uint8_t *)malloc(HEAD + u + 16);
-        if (!b.p) { b.err = "out of host memory"; return b; }
+        Buf &o = outs[fill_i];
+        if (!reserve(o, HEAD + u + 16, 0)) { b.err = "out of host memory"; return b; }
         char e[256] = {0};
-        if (fn(user, comp.data(), p, blks.data(), blks.size(), b.p + HEAD, u, e, sizeof e) != 0) {
-            free(b.p);
-            b.p = nullptr;
+        if (inf->inflate(inf->user, cin.p, p, blks.data(), blks.size(), o.p + HEAD, u, e, sizeof e) != 0) {
             b.err = e[0] ? e : "BGZF inflate failed";
             return b;
         }
-        comp.erase(comp.begin(), comp.begin() + (ptrdiff_t)p);
+        memmove(cin.p, cin.p + p, cin_n - p);   // the partial block left for the next batch
+        cin_n -= p;
+        b.p = o.p;
         b.n = u;
         b.ok = true;
+        fill_i ^= 1;
         return b;
     }
 
     // Device path of next(): the pending batch (or a synchronous first one) becomes the buffer,
-    // the unconsumed tail [at, size) moved in front of it; the batch after it starts.
+    // the unconsumed tail [at, size) moved in front of it; the batch after it starts, into the
+    // output buffer the parser just left.
     bool next_device(Bytes &out, size_t &at) {
         Batch b = pending.valid() ? pending.get() : produce();
         if (!b.ok) { err = b.err; return false; }
-        if (b.n == 0) { free(b.p); return false; }   // end of file
-        pending = std::async(std::launch::async, [this] { return produce(); });
+        if (b.n == 0) return false;   // end of file
         const size_t tail = out.size() - at;
-        if (tail <= HEAD) {
-            memcpy(b.p + HEAD - tail, out.data() + at, tail);
-            out.adopt(b.p, HEAD + b.n, HEAD + b.n + 16);
-            at = HEAD - tail;
-        } else {   // (a record longer than HEAD: append)
-            out.erase_front(at);
-            at = 0;
-            const size_t base = out.size();
-            if (!out.resize(base + b.n)) { free(b.p); err = "out of host memory"; return false; }
-            memcpy(out.data() + base, b.p + HEAD, b.n);
-            free(b.p);
-        }
+        if (tail > HEAD) { err = "a BAM record longer than 64 MiB"; return false; }
+        memcpy(b.p + HEAD - tail, out.data() + at, tail);
+        out.view(b.p, HEAD + b.n);   // (the reader owns the buffer)
+        at = HEAD - tail;
+        pending = std::async(std::launch::async, [this] { return produce(); });
         return true;
     }
 
     // Make more inflated bytes available in out (consumed up to `at`); false at end of file /
     // on error.
     bool next(Bytes &out, size_t &at) {
-        if (fn) return next_device(out, at);
+        if (inf) return next_device(out, at);
         if (at) {
             out.erase_front(at);
             at = 0;
@@ -500,11 +549,11 @@ svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap)
 
 svth_bam *svth_bam_read_region(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
                                char *err, size_t errcap) {
-    return svth_bam_read_ex(path, threads, tid0, beg0, tid1, end1, nullptr, nullptr, err, errcap);
+    return svth_bam_read_ex(path, threads, tid0, beg0, tid1, end1, nullptr, err, errcap);
 }
 
 svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
-                           svth_inflate_fn fn, void *user, char *err, size_t errcap) {
+                           const svth_inflater *inf, char *err, size_t errcap) {
     const bool region = tid0 >= 0;
     auto fail = [&](const std::string &m) -> svth_bam * {
         if (err && errcap) snprintf(err, errcap, "%s", m.c_str());
@@ -515,8 +564,11 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
     BgzfReader rd;
     rd.f = f;
     rd.threads = threads < 1 ? 1 : threads;
-    rd.fn = fn;
-    rd.user = user;
+    rd.inf = inf && inf->inflate ? inf : nullptr;
+    {
+        struct stat st;
+        rd.fsize = fstat(fileno(f), &st) == 0 ? (uint64_t)st.st_size : 0;
+    }
     Bytes buf;
     size_t at = 0;
     auto need = [&](size_t k) -> bool {

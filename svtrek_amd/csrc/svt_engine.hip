@@ -3140,6 +3140,19 @@ svt_status svt_bgzf_inflate(svt_ctx *c, const uint8_t *comp, size_t comp_bytes, 
 
 double svt_bgzf_last_inflate_ms(const svt_ctx *c) { return c ? c->inf_ms : 0.0; }
 
+void *svt_host_alloc(svt_ctx *c, size_t bytes) {
+    if (!c) return nullptr;
+    DevGuard dg(c->device);
+    void *p = nullptr;
+    return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+
+void svt_host_free(svt_ctx *c, void *p) {
+    if (!c || !p) return;
+    DevGuard dg(c->device);
+    (void)hipHostFree(p);
+}
+
 void svt_close(svt_ctx *c) {
     if (!c) return;
     for (svt_ctx *d : c->subs) svt_close(d);

@@ -33,15 +33,24 @@ svth_bam *svth_bam_read(const char *path, int threads, char *err, size_t errcap)
  * included.  tid0 < 0: the whole file (svth_bam_read). */
 svth_bam *svth_bam_read_region(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
                                char *err, size_t errcap);
-/* A BGZF inflater for the ingest (svth_bam_read_ex): inflate n blocks of comp into out (the
- * layout of svt_bgzf_inflate, include/svtrek_gpu.h); 0 = done, else a message in err. */
-typedef int (*svth_inflate_fn)(void *user, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
-                               size_t n, uint8_t *out, size_t out_bytes, char *err, size_t errcap);
-/* svth_bam_read_region with the BGZF blocks inflated by `fn` (the CLI passes the device's
- * svt_bgzf_inflate) in batches of ~1 GiB of compressed input, the next batch read and
- * inflated while the records of the current one are parsed; fn == NULL: host threads. */
+/* A BGZF inflater for the ingest (svth_bam_read_ex): inflate(n blocks of comp -> out, the
+ * layout of svt_bgzf_inflate, include/svtrek_gpu.h; 0 = done, else a message in err); alloc /
+ * release (optional): the buffers inflate reads and writes fastest (pinned host memory);
+ * batch_bytes: compressed bytes per inflate call (0: 1 GiB). */
+typedef struct svth_inflater {
+    int (*inflate)(void *user, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks, size_t n,
+                   uint8_t *out, size_t out_bytes, char *err, size_t errcap);
+    void *(*alloc)(void *user, size_t bytes);
+    void (*release)(void *user, void *p);
+    void *user;
+    size_t batch_bytes;
+} svth_inflater;
+/* svth_bam_read_region with the BGZF blocks inflated by `inf` (the CLI passes the device's
+ * svt_bgzf_inflate and pinned buffers): batches read by `threads` parallel preads, the next
+ * batch read and inflated by a helper thread while the records of the current one are parsed;
+ * inf == NULL: host threads inflate. */
 svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
-                           svth_inflate_fn fn, void *user, char *err, size_t errcap);
+                           const svth_inflater *inf, char *err, size_t errcap);
 void      svth_bam_free(svth_bam *b);
 /* View valid until svth_bam_free. */
 void      svth_bam_view(const svth_bam *b, svt_pileup_view *out);

@@ -240,6 +240,16 @@ struct DeviceInflate {
     const int *open_rc;
     double ms = 0;   // device time of the inflate kernels
 };
+void *device_host_alloc(void *user, size_t bytes) {   // pinned buffers for the ingest's batches
+    DeviceInflate *d = (DeviceInflate *)user;
+    d->ready.wait();
+    return *d->open_rc || !*d->ctx ? malloc(bytes) : svt_host_alloc(*d->ctx, bytes);
+}
+void device_host_free(void *user, void *p) {
+    DeviceInflate *d = (DeviceInflate *)user;
+    if (*d->open_rc || !*d->ctx) free(p);
+    else svt_host_free(*d->ctx, p);
+}
 int device_inflate(void *user, const uint8_t *comp, size_t cb, const svt_bgzf_block *blocks, size_t n, uint8_t *out,
                    size_t ob, char *err, size_t ecap) {
     DeviceInflate *d = (DeviceInflate *)user;
@@ -289,8 +299,9 @@ int audit(int argc, char **argv) {
         t_parse_end = now_s();
     });
     char err[512];
-    svth_bam *bam = svth_bam_read_ex(a.bam, a.threads, -1, 0, -1, 0, a.gpu_inflate ? device_inflate : nullptr, &dinf,
-                                     err, sizeof err);
+    // GPU inflate: ~4 GiB compressed batches (~64K BGZF blocks, one lane each, fill the chip)
+    const svth_inflater dev_inf{device_inflate, device_host_alloc, device_host_free, &dinf, 4ull << 30};
+    svth_bam *bam = svth_bam_read_ex(a.bam, a.threads, -1, 0, -1, 0, a.gpu_inflate ? &dev_inf : nullptr, err, sizeof err);
     const double t_ingest = now_s();
     vt.join();
     ot.join();

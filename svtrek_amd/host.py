@@ -25,7 +25,7 @@ def load_host() -> C.CDLL:
         L.svth_bam_read_region.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int64, C.c_int32, C.c_int64,
                                            C.c_char_p, C.c_size_t]
         L.svth_bam_read_region.restype = P
-        L.svth_bam_read_ex.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int64, C.c_int32, C.c_int64, P, P,
+        L.svth_bam_read_ex.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int64, C.c_int32, C.c_int64, P,
                                        C.c_char_p, C.c_size_t]
         L.svth_bam_read_ex.restype = P
         L.svth_vcf_parse.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
@@ -66,10 +66,17 @@ def load_host() -> C.CDLL:
 
 INFLATE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                          C.c_void_p, C.c_size_t)
+ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_size_t)
+RELEASE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p)
+
+
+class SvthInflater(C.Structure):
+    _fields_ = [("inflate", C.c_void_p), ("alloc", C.c_void_p), ("release", C.c_void_p), ("user", C.c_void_p),
+                ("batch_bytes", C.c_size_t)]
 
 
 def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | None = None,
-             inflate=None) -> tuple[Pileup, dict]:
+             inflate=None, batch_bytes: int = 0) -> tuple[Pileup, dict]:
     """The BAM as a columnar pileup.  region = (tid0, beg0, tid1, end1): only the records from
     the BAI's linear-index offset of (tid0, beg0) up to the first at or past (tid1, end1)
     (svth_bam_read_region; needs `path`.bai) -- what one shard's queries can yield.
@@ -90,7 +97,10 @@ def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | No
                 C.memmove(e, m + b"\0", len(m) + 1)
             return rc
         fn = INFLATE_FN(cb)
-        h = L.svth_bam_read_ex(path.encode(), threads, t0, b0, t1, e1, C.cast(fn, C.c_void_p), None, err, 512)
+        fa = ALLOC_FN(lambda _u, n: lib.svt_host_alloc(ctx, n))
+        fr = RELEASE_FN(lambda _u, p: lib.svt_host_free(ctx, p))
+        inf = SvthInflater(C.cast(fn, C.c_void_p), C.cast(fa, C.c_void_p), C.cast(fr, C.c_void_p), None, batch_bytes)
+        h = L.svth_bam_read_ex(path.encode(), threads, t0, b0, t1, e1, C.byref(inf), err, 512)
     if not h:
         raise OSError(err.value.decode())
     try:

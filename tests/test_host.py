@@ -293,7 +293,7 @@ def test_bam_read_with_inflate_callback(tmp_path, region):
     want, wi = host.read_bam(path, threads=3, region=reg)
     cpu = Engine(Params(), device=0, lib=bind_abi(ctypes.CDLL(os.path.join(ROOT, "oracle", "libsvtrek_cpu.so"))))
     try:
-        got, gi = host.read_bam(path, threads=3, region=reg, inflate=cpu)
+        got, gi = host.read_bam(path, threads=3, region=reg, inflate=cpu, batch_bytes=100_000)   # many batches
     finally:
         cpu.close()
     assert wi == gi
