@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <future>
 #include <cstdio>
 #include <cstdlib>
@@ -142,6 +143,9 @@ struct BgzfReader {
         std::string err;
     };
     std::future<Batch> pending;
+    // stage times (s): read, header scan, buffer allocation, inflate, parser waiting on a batch
+    double t_read = 0, t_scan = 0, t_alloc = 0, t_inflate = 0, t_wait = 0;
+    static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
     ~BgzfReader() {
         drop_pending();
@@ -184,7 +188,15 @@ struct BgzfReader {
     bool read_batch(size_t want) {
         if (foff >= fsize) { eof = true; return true; }
         want = (size_t)std::min<uint64_t>(want, fsize - foff);
+        const double t0 = now();
         if (!reserve(cin, cin_n + want + 64, cin_n)) return false;
+        const double t1 = now();
+        t_alloc += t1 - t0;
+        struct Acc {
+            double &t;
+            double t1;
+            ~Acc() { t += now() - t1; }
+        } acc{t_read, t1};
         const int fd = fileno(f);
         std::atomic<int> bad{0};
         parallel_for(threads, want, [&](size_t a, size_t b) {
@@ -209,6 +221,7 @@ struct BgzfReader {
         const size_t want = inf->batch_bytes ? inf->batch_bytes : (1ull << 30);
         for (;;) {
             if (!eof && !read_batch(want)) { b.err = err; return b; }
+            const double ts = now();
             while (p + 18 <= cin_n) {
                 const uint8_t *h = cin.p + p;
                 if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { b.err = "not a BGZF file (bad gzip header)"; return b; }
@@ -232,6 +245,7 @@ struct BgzfReader {
                 u += k.ulen;
                 p += bsize;
             }
+            t_scan += now() - ts;
             if (!blks.empty() || eof) break;   // (else a single block larger than what was read so far)
         }
         if (blks.empty()) {
@@ -240,9 +254,14 @@ struct BgzfReader {
             return b;
         }
         Buf &o = outs[fill_i];
+        double t0 = now();
         if (!reserve(o, HEAD + u + 16, 0)) { b.err = "out of host memory"; return b; }
+        double t1 = now();
+        t_alloc += t1 - t0;
         char e[256] = {0};
-        if (inf->inflate(inf->user, cin.p, p, blks.data(), blks.size(), o.p + HEAD, u, e, sizeof e) != 0) {
+        const int rc = inf->inflate(inf->user, cin.p, p, blks.data(), blks.size(), o.p + HEAD, u, e, sizeof e);
+        t_inflate += now() - t1;
+        if (rc != 0) {
             b.err = e[0] ? e : "BGZF inflate failed";
             return b;
         }
@@ -259,7 +278,9 @@ struct BgzfReader {
     // the unconsumed tail [at, size) moved in front of it; the batch after it starts, into the
     // output buffer the parser just left.
     bool next_device(Bytes &out, size_t &at) {
+        const double tw = now();
         Batch b = pending.valid() ? pending.get() : produce();
+        t_wait += now() - tw;
         if (!b.ok) { err = b.err; return false; }
         if (b.n == 0) return false;   // end of file
         const size_t tail = out.size() - at;
@@ -539,6 +560,7 @@ struct svth_bam {
     RawVec<uint32_t> cigar;
     RawVec<uint8_t> clip;
     int64_t n_records = 0, n_cg = 0;
+    double stage_s[6] = {0, 0, 0, 0, 0, 0};   // read, scan, alloc, inflate, wait, total
 };
 
 extern "C" {
@@ -559,6 +581,7 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
         if (err && errcap) snprintf(err, errcap, "%s", m.c_str());
         return nullptr;
     };
+    const double t_start = BgzfReader::now();
     FILE *f = fopen(path, "rb");
     if (!f) return fail(std::string("cannot open BAM: ") + path);
     BgzfReader rd;
@@ -701,6 +724,10 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
     rd.drop_pending();
     fclose(f);
     if (!rd.err.empty()) { delete b; return fail(rd.err); }
+    {
+        const double st[6] = {rd.t_read, rd.t_scan, rd.t_alloc, rd.t_inflate, rd.t_wait, BgzfReader::now() - t_start};
+        memcpy(b->stage_s, st, sizeof st);
+    }
     const size_t n = b->pos.size();
     if (!b->cig_off.push_back(narena)) { delete b; return fail("out of host memory"); }
     // per-tid ranges; reorder only when the file was not coordinate-sorted
@@ -756,5 +783,6 @@ const char *svth_bam_target_name(const svth_bam *b, int32_t t) {
 }
 int64_t svth_bam_n_records(const svth_bam *b) { return b->n_records; }
 int64_t svth_bam_n_cg_restored(const svth_bam *b) { return b->n_cg; }
+void svth_bam_stage_seconds(const svth_bam *b, double *s6) { memcpy(s6, b->stage_s, sizeof b->stage_s); }
 
 }  // extern "C"

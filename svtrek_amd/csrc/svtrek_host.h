@@ -58,6 +58,9 @@ int32_t   svth_bam_n_targets(const svth_bam *b);
 const char *svth_bam_target_name(const svth_bam *b, int32_t tid);
 int64_t   svth_bam_n_records(const svth_bam *b);     /* all records incl. tid < 0     */
 int64_t   svth_bam_n_cg_restored(const svth_bam *b); /* CIGARs restored from CG:B,I   */
+/* Where a device-inflate read spent its time (s): batch reads, header scans, buffer allocation,
+ * inflate calls (all on the helper thread), the parser waiting for batches, and the whole read. */
+void      svth_bam_stage_seconds(const svth_bam *b, double *s6);
 
 /* A1: parse one VCF data line in place (as strtok_r does).
  * Returns 1 = record reaches the type switch (*l filled), 0 = skipped silently,

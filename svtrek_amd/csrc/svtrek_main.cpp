@@ -312,6 +312,8 @@ int audit(int argc, char **argv) {
         close_all();
         return 1;
     }
+    double stage[6];
+    svth_bam_stage_seconds(bam, stage);
     svt_pileup_view view;
     svth_bam_view(bam, &view);
     size_t mlen = 0;
@@ -386,7 +388,10 @@ int audit(int argc, char **argv) {
         fprintf(stderr, "[svtrek_amd] ingest %.3fs (inflate %s%s)  vcf-read+parse %.3fs (beside the ingest)  "
                         "load+refine %.3fs (load %.3fs)  print %.3fs  records %zu\n",
                 t_ingest - t0, a.gpu_inflate ? "gpu, kernels " : "cpu",
-                a.gpu_inflate ? (std::to_string(dinf.ms / 1e3).substr(0, 5) + "s").c_str() : "",
+                a.gpu_inflate ? (std::to_string(dinf.ms / 1e3).substr(0, 5) + "s; batch read " +
+                                 std::to_string(stage[0]).substr(0, 5) + "s alloc " + std::to_string(stage[2]).substr(0, 5) +
+                                 "s inflate calls " + std::to_string(stage[3]).substr(0, 5) + "s parser waits " +
+                                 std::to_string(stage[4]).substr(0, 5) + "s").c_str() : "",
                 t_parse_end - t0, t_refine - t_parse, *std::max_element(load_s.begin(), load_s.end()),
                 now_s() - t_refine, loci.size());
     return 0;

@@ -54,6 +54,8 @@ def load_host() -> C.CDLL:
         L.svth_bam_n_records.restype = C.c_int64
         L.svth_bam_n_cg_restored.argtypes = [P]
         L.svth_bam_n_cg_restored.restype = C.c_int64
+        L.svth_bam_stage_seconds.argtypes = [P, P]
+        L.svth_bam_stage_seconds.restype = None
         L.svth_parse_line.argtypes = [C.c_char_p, P, C.c_char_p, C.c_size_t]
         L.svth_parse_line.restype = C.c_int
         L.svth_format.argtypes = [P, P, C.c_char_p, C.c_size_t]
@@ -76,7 +78,7 @@ class SvthInflater(C.Structure):
 
 
 def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | None = None,
-             inflate=None, batch_bytes: int = 0) -> tuple[Pileup, dict]:
+             inflate=None, batch_bytes: int = 0, pinned: bool = True) -> tuple[Pileup, dict]:
     """The BAM as a columnar pileup.  region = (tid0, beg0, tid1, end1): only the records from
     the BAI's linear-index offset of (tid0, beg0) up to the first at or past (tid1, end1)
     (svth_bam_read_region; needs `path`.bai) -- what one shard's queries can yield.
@@ -99,7 +101,8 @@ def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | No
         fn = INFLATE_FN(cb)
         fa = ALLOC_FN(lambda _u, n: lib.svt_host_alloc(ctx, n))
         fr = RELEASE_FN(lambda _u, p: lib.svt_host_free(ctx, p))
-        inf = SvthInflater(C.cast(fn, C.c_void_p), C.cast(fa, C.c_void_p), C.cast(fr, C.c_void_p), None, batch_bytes)
+        inf = SvthInflater(C.cast(fn, C.c_void_p), C.cast(fa, C.c_void_p) if pinned else None,
+                           C.cast(fr, C.c_void_p) if pinned else None, None, batch_bytes)
         h = L.svth_bam_read_ex(path.encode(), threads, t0, b0, t1, e1, C.byref(inf), err, 512)
     if not h:
         raise OSError(err.value.decode())
@@ -123,8 +126,11 @@ def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | No
         pl = Pileup(tid_off=tid_off, pos=arr(v.pos, np.int32, nr), endpos=arr(v.endpos, np.int32, nr),
                     cig_off=cig_off, cigar=arr(v.cigar, np.uint32, int(cig_off[-1])),
                     clip=arr(v.clip, np.uint8, nr))
+        st = (C.c_double * 6)()
+        L.svth_bam_stage_seconds(h, st)
         info = {"names": [L.svth_bam_target_name(h, t).decode() for t in range(nt)],
-                "records": int(L.svth_bam_n_records(h)), "cg_restored": int(L.svth_bam_n_cg_restored(h))}
+                "records": int(L.svth_bam_n_records(h)), "cg_restored": int(L.svth_bam_n_cg_restored(h)),
+                "stage_s": dict(zip(("read", "scan", "alloc", "inflate", "wait", "total"), (round(x, 4) for x in st)))}
         return pl, info
     finally:
         L.svth_bam_free(h)
