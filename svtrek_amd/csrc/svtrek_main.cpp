@@ -300,7 +300,9 @@ int audit(int argc, char **argv) {
     });
     char err[512];
     // GPU inflate: ~4 GiB compressed batches (~64K BGZF blocks, one lane each, fill the chip)
-    const svth_inflater dev_inf{device_inflate, device_host_alloc, device_host_free, &dinf, 4ull << 30};
+    size_t batch_mb = 4096;
+    if (const char *x = getenv("SVTREK_INFLATE_BATCH_MB")) batch_mb = std::max<size_t>(16, strtoull(x, nullptr, 10));
+    const svth_inflater dev_inf{device_inflate, device_host_alloc, device_host_free, &dinf, batch_mb << 20};
     svth_bam *bam = svth_bam_read_ex(a.bam, a.threads, -1, 0, -1, 0, a.gpu_inflate ? &dev_inf : nullptr, err, sizeof err);
     const double t_ingest = now_s();
     vt.join();
