@@ -132,9 +132,20 @@ struct BgzfReader {
         uint8_t *p = nullptr;
         size_t cap = 0;
     };
-    Buf cin, outs[2];     // compressed input; output buffers (one parsed, one being filled)
-    size_t cin_n = 0;     // bytes held in cin (a partial block left from the previous batch first)
-    int fill_i = 0;       // the output buffer the next batch goes to
+    Buf cins[2], outs[2];  // compressed input (one inflated, one being read); output (one parsed, one filled)
+    size_t cin_n[2] = {0, 0};
+    int read_i = 0, fill_i = 0;   // the input / output buffer the next batch goes to
+    // the partial block at the end of the last batch read: cins[carry_i][carry_p, +carry_n)
+    int carry_i = 0;
+    size_t carry_p = 0, carry_n = 0;
+    struct Comp {                 // a batch read and scanned: its blocks in cins[i][0, p)
+        int i = 0;
+        size_t p = 0, u = 0;
+        std::vector<svt_bgzf_block> blks;
+        bool ok = false;
+        std::string err;
+    };
+    std::future<Comp> pending_comp;
     uint64_t foff = 0, fsize = 0;
     struct Batch {
         uint8_t *p = nullptr;   // outs[i].p: HEAD bytes, then n inflated bytes
@@ -143,16 +154,18 @@ struct BgzfReader {
         std::string err;
     };
     std::future<Batch> pending;
-    // stage times (s): read, header scan, buffer allocation, inflate, parser waiting on a batch
-    double t_read = 0, t_scan = 0, t_alloc = 0, t_inflate = 0, t_wait = 0;
+    // stage times (s): read, header scan, buffer allocation (reader, inflater), inflate, parser
+    // waiting on a batch
+    double t_read = 0, t_scan = 0, t_alloc_r = 0, t_alloc = 0, t_inflate = 0, t_wait = 0;
     static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
     ~BgzfReader() {
         drop_pending();
-        for (Buf *b : {&cin, &outs[0], &outs[1]}) release(*b);
+        for (Buf *b : {&cins[0], &cins[1], &outs[0], &outs[1]}) release(*b);
     }
     void drop_pending() {
         if (pending.valid()) (void)pending.get();
+        if (pending_comp.valid()) (void)pending_comp.get();
     }
     void release(Buf &b) {
         if (b.p) {
@@ -177,56 +190,65 @@ struct BgzfReader {
     bool seek(uint64_t coff) {
         drop_pending();
         comp.clear();
-        cin_n = 0;
+        cin_n[0] = cin_n[1] = 0;
+        carry_n = 0;
         foff = coff;
         eof = false;
         if (fseeko(f, (off_t)coff, SEEK_SET) != 0) { err = "cannot seek in BAM (BAI offset past the end?)"; return false; }
         return true;
     }
 
-    // Read the next batch of compressed bytes after what cin holds, `threads` preads at once.
-    bool read_batch(size_t want) {
+    // Append the next ~want compressed bytes to buffer b (holding n), `threads` preads at once.
+    bool read_batch(Buf &b, size_t &n, size_t want) {
         if (foff >= fsize) { eof = true; return true; }
         want = (size_t)std::min<uint64_t>(want, fsize - foff);
         const double t0 = now();
-        if (!reserve(cin, cin_n + want + 64, cin_n)) return false;
+        if (!reserve(b, n + want + 64, n)) { err = "out of host memory"; return false; }
         const double t1 = now();
-        t_alloc += t1 - t0;
-        struct Acc {
-            double &t;
-            double t1;
-            ~Acc() { t += now() - t1; }
-        } acc{t_read, t1};
+        t_alloc_r += t1 - t0;
         const int fd = fileno(f);
         std::atomic<int> bad{0};
-        parallel_for(threads, want, [&](size_t a, size_t b) {
-            for (size_t o = a; o < b;) {
-                const ssize_t r = pread(fd, cin.p + cin_n + o, b - o, (off_t)(foff + o));
+        uint8_t *dst = b.p + n;
+        const uint64_t at = foff;
+        parallel_for(threads, want, [&](size_t a, size_t e) {
+            for (size_t o = a; o < e;) {
+                const ssize_t r = pread(fd, dst + o, e - o, (off_t)(at + o));
                 if (r <= 0) { bad = 1; return; }
                 o += (size_t)r;
             }
         });
+        t_read += now() - t1;
         if (bad) { err = "cannot read BAM"; return false; }
-        cin_n += want;
+        n += want;
         foff += want;
         if (foff >= fsize) eof = true;
         return true;
     }
 
-    // Read and inflate the next batch (helper thread); ok && n == 0 at end of file.
-    Batch produce() {
-        Batch b;
-        std::vector<svt_bgzf_block> blks;
-        size_t p = 0, u = 0;
+    // Read and scan the next batch into cins[read_i] (the previous batch's partial block first).
+    Comp read_next() {
+        Comp c;
+        c.i = read_i;
+        Buf &b = cins[read_i];
+        size_t &n = cin_n[read_i];
         const size_t want = inf->batch_bytes ? inf->batch_bytes : (1ull << 30);
+        n = 0;
+        if (carry_n) {
+            const double t0 = now();
+            if (!reserve(b, carry_n + want + 64, 0)) { c.err = "out of host memory"; return c; }
+            t_alloc_r += now() - t0;
+            memcpy(b.p, cins[carry_i].p + carry_p, carry_n);
+            n = carry_n;
+        }
+        size_t p = 0, u = 0;
         for (;;) {
-            if (!eof && !read_batch(want)) { b.err = err; return b; }
+            if (!eof && !read_batch(b, n, want)) { c.err = err; return c; }
             const double ts = now();
-            while (p + 18 <= cin_n) {
-                const uint8_t *h = cin.p + p;
-                if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { b.err = "not a BGZF file (bad gzip header)"; return b; }
+            while (p + 18 <= n) {
+                const uint8_t *h = b.p + p;
+                if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { c.err = "not a BGZF file (bad gzip header)"; return c; }
                 const uint16_t xlen = rd16(h + 10);
-                if (p + 12 + xlen > cin_n) break;
+                if (p + 12 + xlen > n) break;
                 size_t bsize = 0;
                 for (size_t x = 0; x + 4 <= xlen;) {
                     const uint8_t *sf = h + 12 + x;
@@ -234,41 +256,53 @@ struct BgzfReader {
                     if (sf[0] == 66 && sf[1] == 67 && slen == 2) bsize = (size_t)rd16(sf + 4) + 1;
                     x += 4 + slen;
                 }
-                if (!bsize || bsize < (size_t)xlen + 20) { b.err = "BGZF block without BC subfield"; return b; }
-                if (p + bsize > cin_n) break;
+                if (!bsize || bsize < (size_t)xlen + 20) { c.err = "BGZF block without BC subfield"; return c; }
+                if (p + bsize > n) break;
                 svt_bgzf_block k;
                 k.coff = p + 12 + xlen;
                 k.clen = (uint32_t)(bsize - xlen - 20);
                 k.uoff = u;
-                k.ulen = rd32(cin.p + p + bsize - 4);
-                blks.push_back(k);
+                k.ulen = rd32(b.p + p + bsize - 4);
+                c.blks.push_back(k);
                 u += k.ulen;
                 p += bsize;
             }
             t_scan += now() - ts;
-            if (!blks.empty() || eof) break;   // (else a single block larger than what was read so far)
+            if (!c.blks.empty() || eof) break;   // (else a single block larger than what was read so far)
         }
-        if (blks.empty()) {
-            if (cin_n) { b.err = "truncated BGZF block at end of file"; return b; }
-            b.ok = true;
-            return b;
-        }
+        if (c.blks.empty() && n) { c.err = "truncated BGZF block at end of file"; return c; }
+        c.p = p;
+        c.u = u;
+        c.ok = true;
+        carry_i = read_i;
+        carry_p = p;
+        carry_n = n - p;
+        read_i ^= 1;
+        return c;
+    }
+
+    // Inflate the next batch (helper thread), the batch after it being read meanwhile; ok && n ==
+    // 0 at end of file.
+    Batch produce() {
+        Batch b;
+        Comp c = pending_comp.valid() ? pending_comp.get() : read_next();
+        if (!c.ok) { b.err = c.err; return b; }
+        if (c.blks.empty()) { b.ok = true; return b; }   // end of file
+        if (!eof || carry_n) pending_comp = std::async(std::launch::async, [this] { return read_next(); });
         Buf &o = outs[fill_i];
         double t0 = now();
-        if (!reserve(o, HEAD + u + 16, 0)) { b.err = "out of host memory"; return b; }
+        if (!reserve(o, HEAD + c.u + 16, 0)) { b.err = "out of host memory"; return b; }
         double t1 = now();
         t_alloc += t1 - t0;
         char e[256] = {0};
-        const int rc = inf->inflate(inf->user, cin.p, p, blks.data(), blks.size(), o.p + HEAD, u, e, sizeof e);
+        const int rc = inf->inflate(inf->user, cins[c.i].p, c.p, c.blks.data(), c.blks.size(), o.p + HEAD, c.u, e, sizeof e);
         t_inflate += now() - t1;
         if (rc != 0) {
             b.err = e[0] ? e : "BGZF inflate failed";
             return b;
         }
-        memmove(cin.p, cin.p + p, cin_n - p);   // the partial block left for the next batch
-        cin_n -= p;
         b.p = o.p;
-        b.n = u;
+        b.n = c.u;
         b.ok = true;
         fill_i ^= 1;
         return b;
@@ -725,7 +759,8 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
     fclose(f);
     if (!rd.err.empty()) { delete b; return fail(rd.err); }
     {
-        const double st[6] = {rd.t_read, rd.t_scan, rd.t_alloc, rd.t_inflate, rd.t_wait, BgzfReader::now() - t_start};
+        const double st[6] = {rd.t_read, rd.t_scan, rd.t_alloc_r + rd.t_alloc, rd.t_inflate, rd.t_wait,
+                              BgzfReader::now() - t_start};
         memcpy(b->stage_s, st, sizeof st);
     }
     const size_t n = b->pos.size();

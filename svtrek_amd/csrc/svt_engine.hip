@@ -2006,11 +2006,6 @@ struct svt_ctx {
     IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan
     uint32_t *d_xlist = nullptr;      // [n_ranges] ranges for the exact census
     uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
-    IxTot *d_gagg = nullptr, *d_gincl = nullptr;   // [n_groups] the fused build's look-back chain
-    uint32_t *d_gflag = nullptr;
-    unsigned long long *d_gctr = nullptr, gctr_base = 0;
-    uint32_t ix_epoch = 0;            // fused builds so far (the chain's flags carry it)
-    bool ix_fused = true;             // rebuilds of the lane index in one kernel (SVTREK_IX_FUSED=0: two)
     uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
     int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
                                       // walk (svt_index.inc) -- SVTREK_IX=auto|lane|stream
@@ -2129,8 +2124,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_cnt); hfree(c->d_gagg); hfree(c->d_gincl); hfree(c->d_gflag); hfree(c->d_gctr);
-    c->gctr_base = 0; hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
+    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
     hfree(c->d_lchunk);
     c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
@@ -2399,7 +2393,6 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     const char *g = getenv("SVTREK_GATHER");   // "span1": the one-wave-per-window kernel at every batch size
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *x = getenv("SVTREK_IX_EXACT")) c->ix_exact = atoi(x) == 1;
-    if (const char *x = getenv("SVTREK_IX_FUSED")) c->ix_fused = atoi(x) != 0;
     if (const char *x = getenv("SVTREK_IX")) c->ix_mode = strcmp(x, "lane") == 0 ? 1 : strcmp(x, "stream") == 0 ? 2 : 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
@@ -2519,28 +2512,6 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     const uint32_t nparts = lane ? c->n_groups : c->n_ranges;   // what the scan runs over
     Ix2Args a2{a, c->d_cnt, (uint64_t)c->n_reads, c->n_groups};
     const dim3 grid2((unsigned)((c->n_groups + IX2_WPB - 1) / IX2_WPB)), block2(64 * IX2_WPB);
-    if (lane && !first && c->ix_fused) {   // a rebuild: census + look-back + emit in one kernel
-        Ix2Chain ch{c->d_gagg, c->d_gincl, c->d_gflag, c->d_gctr, c->gctr_base, ++c->ix_epoch, c->d_tot,
-                    (uint64_t)c->n_reads};
-        if ((c->ix_epoch >> 30) != 0) {   // (the flags hold 30 bits of it: start over)
-            HIP_TRY(c, hipMemsetAsync(c->d_gflag, 0, (size_t)c->n_groups * sizeof(uint32_t), st));
-            c->ix_epoch = ch.epoch = 1;
-        }
-        c->gctr_base += (unsigned long long)grid2.x * IX2_WPB;   // every wave of the launch takes a number
-        if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
-        hipLaunchKernelGGL(ix2_fused_kernel, grid2, block2, 0, st, a2, ch);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index build: %s", hipGetErrorString(e)));
-        if (ms) {
-            float t0 = 0.f;
-            e = hipEventRecord(ev[1], st);
-            if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
-            if (e == hipSuccess) e = hipEventElapsedTime(&t0, ev[0], ev[1]);
-            if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index timing: %s", hipGetErrorString(e)));
-            *ms = (double)t0;
-        }
-        return done(SVT_OK);
-    }
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     if (lane) {
         hipLaunchKernelGGL(ix2_census_kernel, grid2, block2, 0, st, a2);
@@ -2739,14 +2710,6 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, S))) return s;
     if ((s = upload<uint2>(c, c->d_cnt, nullptr, 0, std::max<size_t>((size_t)nr, 1)))) return s;
-    {
-        const size_t G = std::max<size_t>((size_t)c->n_groups, 1);
-        if ((s = upload<IxTot>(c, c->d_gagg, nullptr, 0, G)) || (s = upload<IxTot>(c, c->d_gincl, nullptr, 0, G)) ||
-            (s = upload<uint32_t>(c, c->d_gflag, nullptr, 0, G)) || (s = upload<unsigned long long>(c, c->d_gctr, nullptr, 0, 1)))
-            return s;
-        c->gctr_base = 0;
-        c->ix_epoch = 0;
-    }
     const size_t NR = std::max<size_t>({(size_t)c->n_ranges, (size_t)c->n_groups, (size_t)1});
     if ((s = upload<IxTot>(c, c->d_agg, nullptr, 0, NR))) return s;
     if ((s = upload<IxTot>(c, c->d_wbase, nullptr, 0, NR))) return s;

@@ -11,6 +11,7 @@
 // queries can reach; one host thread and one svt_ctx per device),
 // print (A11).
 #include <getopt.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <chrono>
@@ -57,12 +58,13 @@ void audt_usage() {
     printf("    --devices <i,j,...>               Explicit GPU per shard (overrides --gpus/--device)\n");
     printf("    --batch <num>                     Records per GPU launch [Default: 1048576]\n");
     printf("    --spill-bytes <num>               Initial candidate spill pool per GPU; grown on demand [Default: 67108864]\n");
-    printf("    --inflate <gpu|cpu>               BGZF decompression of the BAM: first GPU or -t host threads [Default: gpu]\n");
+    printf("    --inflate <auto|gpu|cpu>          BGZF decompression of the BAM: first GPU or -t host threads;\n");
+    printf("                                      auto: the GPU from 1 GiB of BAM on [Default: auto]\n");
 }
 
 struct Args {
     const char *bam = nullptr, *vcf = nullptr, *out = "svtrek.out";
-    int threads = THREADS, verbose = 0, gpus = 1, device = 0, gpu_inflate = 1;
+    int threads = THREADS, verbose = 0, gpus = 1, device = 0, gpu_inflate = -1;   // -1: by BAM size
     size_t batch = 1u << 20;
     std::vector<int> devices;   // device of shard g
     svt_params prm{WIDER, MEDIAN, NARROW, CI_RANGE, CI, MIN_COUNT, 0};
@@ -119,8 +121,11 @@ Args parse_audt(int argc, char **argv) {
         case 22: a.batch = (size_t)strtoull(optarg, nullptr, 10); break;
         case 24: a.prm.spill_bytes = (uint64_t)strtoull(optarg, nullptr, 10); break;
         case 25:
-            if (strcmp(optarg, "gpu") && strcmp(optarg, "cpu")) { fprintf(stderr, "[ERROR] --inflate expects gpu or cpu\n"); exit(EXIT_FAILURE); }
-            a.gpu_inflate = strcmp(optarg, "gpu") == 0;
+            if (strcmp(optarg, "gpu") && strcmp(optarg, "cpu") && strcmp(optarg, "auto")) {
+                fprintf(stderr, "[ERROR] --inflate expects auto, gpu or cpu\n");
+                exit(EXIT_FAILURE);
+            }
+            a.gpu_inflate = strcmp(optarg, "gpu") == 0 ? 1 : strcmp(optarg, "cpu") == 0 ? 0 : -1;
             break;
         case 23: {
             a.devices.clear();
@@ -145,6 +150,10 @@ Args parse_audt(int argc, char **argv) {
     // The reference deadlocks on -t 0 and reads locations[-1] for min-count <= 0.
     if (a.threads < 1) { fprintf(stderr, "[ERROR] -t must be >= 1\n"); exit(EXIT_FAILURE); }
     if (a.prm.consensus_min_count < 1) { fprintf(stderr, "[ERROR] --consensus-min-count must be >= 1\n"); exit(EXIT_FAILURE); }
+    if (a.gpu_inflate < 0) {   // auto: small BAMs inflate faster on the host than the HIP start-up takes
+        struct stat st;
+        a.gpu_inflate = stat(a.bam, &st) == 0 && st.st_size >= (off_t)(1ll << 30) ? 1 : 0;
+    }
     if (a.gpus < 1) a.gpus = 1;
     if (a.batch < 1) a.batch = 1;
     if (a.devices.empty())
@@ -299,9 +308,10 @@ int audit(int argc, char **argv) {
         t_parse_end = now_s();
     });
     char err[512];
-    // GPU inflate: ~4 GiB compressed batches (~64K BGZF blocks, one lane each, fill the chip)
-    size_t batch_mb = 4096;
-    if (const char *x = getenv("SVTREK_INFLATE_BATCH_MB")) batch_mb = std::max<size_t>(16, strtoull(x, nullptr, 10));
+    // GPU inflate: 1 GiB compressed batches (~21K BGZF blocks, one lane each; larger batches
+    // inflate faster but pinning their buffers costs more: cfg2 e2e 5.4 s at 1 GiB, 9.0 s at 4 GiB)
+    size_t batch_mb = 1024;
+    if (const char *x = getenv("SVTREK_INFLATE_BATCH_MB")) batch_mb = std::max<size_t>(1, strtoull(x, nullptr, 10));
     const svth_inflater dev_inf{device_inflate, device_host_alloc, device_host_free, &dinf, batch_mb << 20};
     svth_bam *bam = svth_bam_read_ex(a.bam, a.threads, -1, 0, -1, 0, a.gpu_inflate ? &dev_inf : nullptr, err, sizeof err);
     const double t_ingest = now_s();

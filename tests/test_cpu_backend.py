@@ -57,9 +57,13 @@ def test_cpu_backend_errors():
             e.refine(make_loci([(2, 1, 1000, 5000)]))   # before load_pileup: SVT_ESTATE
 
 
-def test_cli_on_cpu_backend(tmp_path):
+@pytest.mark.parametrize("inflate", ["cpu", "gpu"])
+def test_cli_on_cpu_backend(tmp_path, inflate, monkeypatch):
     """The drop-in CLI's whole flow (BAM ingest, parallel A1 parse beside it, batched refine,
-    batch A11 print) linked against the CPU backend: stdout bytes equal the oracle's."""
+    batch A11 print) linked against the CPU backend: stdout bytes equal the oracle's.
+    --inflate gpu runs the ingest's batch pipeline (here through the CPU backend's
+    svt_bgzf_inflate, zlib) in 1 MiB batches."""
+    monkeypatch.setenv("SVTREK_INFLATE_BATCH_MB", "1")
     r = sim.generate(sim.SimConfig(seed=41, n_targets=2, n_loci=150, del_frac=0.5, coverage=10), keep_handle=True)
     bam = str(tmp_path / "c.bam")
     sim.write_bam(r, bam, with_seq=True, level=1)
@@ -67,7 +71,7 @@ def test_cli_on_cpu_backend(tmp_path):
     sim.write_vcf(r.loci, str(vcf))
     with open(vcf, "a") as f:
         f.write("1\t5000\t.\tA\t<DUP>\t.\tPASS\tSVTYPE=DUP;END=9000\n1\tx\n")
-    p = subprocess.run([CPU_CLI, "audt", "-b", bam, "-v", str(vcf), "-t", "3"], stdout=subprocess.PIPE,
+    p = subprocess.run([CPU_CLI, "audt", "-b", bam, "-v", str(vcf), "-t", "3", "--inflate", inflate], stdout=subprocess.PIPE,
                        stderr=subprocess.PIPE, timeout=300)
     assert p.returncode == 0, p.stderr.decode()
     assert p.stdout.decode("latin-1") == O.audit_text(vcf.read_text(encoding="latin-1"), r.pileup)

@@ -23,8 +23,13 @@ def run_cli(*args, check=True):
     return r
 
 
-def test_cfg1_simvcf_layout(tmp_path):
-    """BASELINE config 1: 100 DEL via the simvcf transform + 10x long-read BAM, -t 1."""
+@pytest.mark.parametrize("inflate", ["auto", "gpu", "gpu-small-batches"])
+def test_cfg1_simvcf_layout(tmp_path, inflate, monkeypatch):
+    """BASELINE config 1: 100 DEL via the simvcf transform + 10x long-read BAM, -t 1; the BAM's
+    BGZF blocks inflated on the host (auto: a small BAM) or on the GPU (also in 16 MiB batches:
+    many batches, partial blocks carried across them)."""
+    if inflate == "gpu-small-batches":
+        monkeypatch.setenv("SVTREK_INFLATE_BATCH_MB", "16")
     r = sim.generate(sim.WORKLOADS["cfg1_100del_10x"], keep_handle=True)
     bam = str(tmp_path / "cfg1.bam")
     sim.write_bam(r, bam, with_seq=True)
@@ -32,7 +37,7 @@ def test_cfg1_simvcf_layout(tmp_path):
     vcf_text = "".join(simulate(resolved, random.Random(101)))
     vcf = tmp_path / "cfg1.sim.vcf"
     vcf.write_text(vcf_text)
-    out = run_cli("-b", bam, "-v", str(vcf), "-t", "1").stdout
+    out = run_cli("-b", bam, "-v", str(vcf), "-t", "1", "--inflate", inflate.split("-")[0]).stdout
     want = O.audit_text(vcf_text, r.pileup)
     assert out == want
     dels = [l for l in out.splitlines() if l.startswith("(DEL)")]

@@ -463,8 +463,8 @@ def test_size_based_kernel_pick_alternating(engine_factory):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_index_census_streaming_vs_exact(engine_factory, seed):
-    """The index builds agree: lane per read (the product's for short reads; rebuilds in one
-    kernel with a look-back chain, or in two with SVTREK_IX_FUSED=0), the stream walk
+    """The index builds agree: lane per read (the product's pick for short reads; also forced),
+    the stream walk
     (SVTREK_IX=stream: ranges whose op lengths cannot reach a slow walk take the streaming
     census, the others the exact per-slot census) and the stream walk with every range forced
     through the exact census (SVTREK_IX_EXACT=1).  A pileup with slow reads in a few places (so
@@ -489,14 +489,14 @@ def test_index_census_streaming_vs_exact(engine_factory, seed):
     loci = random_loci(rng, 400, 1, pos + 2000, hot)
     want = O.refine_batch(pl, loci)
     stats = []
-    for env in (None, {"SVTREK_IX_FUSED": "0"}, {"SVTREK_IX": "stream"},
+    for env in (None, {"SVTREK_IX": "lane"}, {"SVTREK_IX": "stream"},
                 {"SVTREK_IX": "stream", "SVTREK_IX_EXACT": "1"}):
         eng = engine_factory(env=env)
         eng.load_pileup(pl)
         st = eng.load_stats()
         stats.append((st["span_events"], st["lead_blocks"], st["slow_reads"]))
         _assert_same(eng.refine(loci), want, loci)
-        for _ in range(3):   # rebuilds (the lane index's single-pass kernel: epochs of its look-back chain)
+        for _ in range(2):   # rebuilds from the resident pileup
             eng.reindex()
             _assert_same(eng.refine(loci), want, loci)
     assert stats[0] == stats[1] == stats[2] == stats[3] and stats[0][2] >= 4
