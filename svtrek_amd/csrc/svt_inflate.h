@@ -259,15 +259,35 @@ SVT_HD int inf_block(const InfV4 *in, uint32_t skip, uint32_t clen, uint8_t *out
                 if (!inf_build(S.len, 288, F.lit, IF_LB, S.lcnt, S.lsym, S.offs)) return INF_EDATA;
                 if (!inf_build(S.len + 288, ndist, F.dst, IF_DB, S.dcnt, S.dsym, S.offs)) return INF_EDATA;
             }
+            // literals are combined into 4-byte stores at 4-byte aligned output addresses (wc holds
+            // the wn bytes of the current word, from out[op - wn]); a match or the block's end
+            // flushes them first (the copy reads them back)
+            uint32_t wc = 0, wn = 0;
+            auto flush = [&]() {
+                for (uint32_t i = 0; i < wn; i++) out[op - wn + i] = (uint8_t)(wc >> (8 * i));
+                wc = 0;
+                wn = 0;
+            };
             for (;;) {   // literals / lengths until end of block
                 br.fill();
                 const int s = inf_decode(br, F.lit, IF_LB, S.lcnt, S.lsym);
                 if (s < 256) {
                     if (s < 0) return INF_EDATA;
                     if (op >= ulen) return INF_EOUT;
-                    out[op++] = (uint8_t)s;
+                    if (wn == 0 && (((uintptr_t)(out + op)) & 3u) != 0u) {
+                        out[op++] = (uint8_t)s;   // (not yet at a word boundary)
+                        continue;
+                    }
+                    wc |= (uint32_t)s << (8 * wn);
+                    op++;
+                    if (++wn == 4) {
+                        *reinterpret_cast<uint32_t *>(out + op - 4) = wc;
+                        wc = 0;
+                        wn = 0;
+                    }
                     continue;
                 }
+                flush();
                 if (s == 256) break;
                 const int li = s - 257;
                 if (li >= 29) return INF_EDATA;
