@@ -298,22 +298,14 @@ SVT_HD int inf_block(const InfV4 *in, uint32_t skip, uint32_t clen, uint8_t *out
                 const uint32_t dist = inf_dbase(d) + br.get(inf_dext(d));
                 if (dist > op) return INF_EDATA;
                 if (op + len > ulen) return INF_EOUT;
-                // up to 8 bytes a step when the source cannot overlap them: the step's loads are
-                // issued before its stores, one round trip to the cache (BAM data: ~2/3 of the
-                // output comes from matches, most of them 3-4 bytes long from far back)
                 uint32_t k = 0;
-                if (dist >= 8)
-                    while (k < len) {
-                        const uint32_t m = len - k < 8u ? len - k : 8u;
+                if (dist >= 8)   // 8 bytes a step: the loads of a step issued before its stores
+                    for (; k + 8 <= len; k += 8, op += 8) {
                         uint8_t t[8];
 #pragma unroll
-                        for (uint32_t i = 0; i < 8; i++)
-                            if (i < m) t[i] = out[op - dist + i];
+                        for (int i = 0; i < 8; i++) t[i] = out[op - dist + i];
 #pragma unroll
-                        for (uint32_t i = 0; i < 8; i++)
-                            if (i < m) out[op + i] = t[i];
-                        op += m;
-                        k += m;
+                        for (int i = 0; i < 8; i++) out[op + i] = t[i];
                     }
                 for (; k < len; k++, op++) out[op] = out[op - dist];
             }
