@@ -111,7 +111,11 @@ def main() -> int:
                     "method": "sum over the step's kernels of each kernel's median bytes per launch (one launch "
                               "of each per bench.py step)", "source": f"{a.dst}/pmc_*.csv"})
     # profiles/traffic.json: one entry per (engine version, workload, kernel, records)
-    tpath = os.path.join(os.path.dirname(a.dst.rstrip("/")), "traffic.json")
+    # profiles/traffic.json: the profiles/ directory above dst (dst may be nested: profiles/TAG/cfg)
+    d = os.path.abspath(a.dst)
+    while os.path.basename(d) != "profiles" and os.path.dirname(d) != d:
+        d = os.path.dirname(d)
+    tpath = os.path.join(d if os.path.basename(d) == "profiles" else os.path.dirname(os.path.abspath(a.dst)), "traffic.json")
     try:
         with open(tpath) as f:
             old = json.load(f)
