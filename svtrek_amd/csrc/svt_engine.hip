@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_inflate.h"
 
-#define SVT_VERSION "svtrek_amd 0.16.4 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
+#define SVT_VERSION "svtrek_amd 0.16.3 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
 
 namespace {
 
@@ -2006,8 +2006,6 @@ struct svt_ctx {
     IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan
     uint32_t *d_xlist = nullptr;      // [n_ranges] ranges for the exact census
     uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
-    uint32_t *d_slotw = nullptr;      // the stream walk's census slot words (svt_index.inc ix_sbase)
-    uint64_t n_slotw = 0;
     uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
     int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
                                       // walk (svt_index.inc) -- SVTREK_IX=auto|lane|stream
@@ -2126,7 +2124,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_cnt); hfree(c->d_slotw); c->n_slotw = 0; hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
+    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
     hfree(c->d_lchunk);
     c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
@@ -2493,8 +2491,6 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.capL = c->lchunk_units * 4u;
     a.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
     a.xlist = c->d_xlist;
-    a.slotw = c->d_slotw;
-    a.n_slotw = c->n_slotw;
     a.xcnt = (uint32_t *)(c->d_ctl + CTL_XCNT);
     a.exact_all = c->ix_exact ? 1u : 0u;
     a.n_ranges = c->n_ranges;
@@ -2714,8 +2710,6 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, S))) return s;
     if ((s = upload<uint2>(c, c->d_cnt, nullptr, 0, std::max<size_t>((size_t)nr, 1)))) return s;
-    c->n_slotw = (nstream >> 8) + 2ull * c->n_ranges + 8u;   // ix_sbase's layout
-    if ((s = upload<uint32_t>(c, c->d_slotw, nullptr, 0, (size_t)c->n_slotw))) return s;
     const size_t NR = std::max<size_t>({(size_t)c->n_ranges, (size_t)c->n_groups, (size_t)1});
     if ((s = upload<IxTot>(c, c->d_agg, nullptr, 0, NR))) return s;
     if ((s = upload<IxTot>(c, c->d_wbase, nullptr, 0, NR))) return s;
