@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_inflate.h"
 
-#define SVT_VERSION "svtrek_amd 0.16.5 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
+#define SVT_VERSION "svtrek_amd 0.16.6 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
 
 namespace {
 
