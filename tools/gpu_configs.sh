@@ -16,9 +16,11 @@ run() {  # name, timeout, args...
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
   tail -1 "$OUT/$name.log" | cut -c1-400
 }
+if [ -z "${CONFIGS_ONLY:-}" ]; then   # CONFIGS_ONLY=1: the BASELINE workloads only
 run cfg4_shard8_r0 300 --emulate-shard 8:0 --steps 20 --warmup 3 --no-cpu-baseline
 run cfg4_shard8_r7 300 --emulate-shard 8:7 --steps 20 --warmup 3 --no-cpu-baseline
 run cfg4_scale0125 300 --scale 0.125 --steps 20 --warmup 3 --no-cpu-baseline
+fi
 run cfg3 300 --workload cfg3_50k_delins_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
 run cfg2 300 --workload cfg2_10kdel_30x_ont --steps 20 --warmup 3 --no-cpu-baseline
 run cfg1 200 --workload cfg1_100del_10x --steps 20 --warmup 3 --no-cpu-baseline
