@@ -23,15 +23,19 @@ A step is the whole per-locus path from the resident columnar pileup to refined 
      overlaps step i + 1; double-buffered records).
 Rank 0 prints ONE JSON line.
 
-roofline: `achieved` = SURVEY.md §8(d)'s algorithmic bytes of the step -- what the reference's
-per-window CIGAR walk touches, 24 B/locus + 12 B/yielded read + 4 B/CIGAR word walked, counted
-exactly by svt_count_work -- / the step's mean duration from HIP events on the launch stream.
-`phases` splits the step (index build, refine) with their own event timings, and
-`engine_bytes` prices the refine launch alone with the span walk's own bytes (svt_work
-.event_bytes).  `traffic` = HBM bytes per step from the committed rocprofv3 PMC passes of this
-engine version and workload, summed over the step's kernels (profiles/traffic.json,
-tools/make_traffic.py).  cpu_baseline: the CPU oracle (restatement of the reference's tpool
-path) on rank 0's host cores.
+roofline (HBM-bound integer work, no MFMA): `achieved` = the step's algorithmic bytes -- what
+the engine's own algorithm must move: the index build's (svt_load_stats.index_bytes: the CIGAR
+stream twice, per-read records and offsets, the span events written) plus the refine launch's
+(svt_work.event_bytes: loci, region queries, span bounds and events, 16-B result records) -- / the
+step's mean duration from HIP events on the launch stream; `frac` = achieved / 8 TB/s.
+`traffic` = the HBM bytes per step the rocprofv3 PMC passes of this engine version and workload
+measured (profiles/traffic.json, tools/make_traffic.py), `frac_hbm` = traffic / step / 8 TB/s,
+and `kernels` the same per kernel ({ms from the committed --stats summary, bytes, frac}).
+`reference_equivalent` prices the step with SURVEY.md §8(d)'s bytes instead -- what the
+reference's per-window CIGAR walk touches (24 B/locus + 12 B/yielded read + 4 B/CIGAR word walked,
+svt_count_work): the engine walks each read once where the reference re-walks it per window, so
+that rate is an effective one and may pass the peak.  cpu_baseline: the CPU oracle (restatement
+of the reference's tpool path) on rank 0's host cores.
 """
 from __future__ import annotations
 
@@ -128,22 +132,20 @@ def _engine_version() -> str:
 
 
 STEP_KERNELS = ("ix2_census_kernel", "ix2_emit_kernel", "refine_lane_kernel", "refine_redo_kernel")
-STREAM_INDEX_KERNELS = ("ix_census_kernel", "index_kernel<emit>")   # the long-read index build (svt_index.inc)
+STREAM_INDEX_KERNELS = ("ix_census_kernel", "index_kernel")   # the long-read index build (svt_index.inc)
 
 
-def _traffic(workload: str, kernel: str, records: bool) -> tuple[int | None, str | None]:
-    """HBM bytes per step of this engine version / workload from the committed rocprofv3 PMC
-    passes (tools/make_traffic.py -> profiles/traffic.json), or (None, None)."""
+def _traffic(workload: str, records: bool) -> dict:
+    """kernel -> profiles/traffic.json entry (HBM bytes per launch from the committed rocprofv3
+    PMC passes, tools/make_traffic.py; "step" = their sum) for this engine version / workload."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
     except (OSError, ValueError):
-        return None, None
-    for e in tj if isinstance(tj, list) else [tj]:
-        if (e.get("engine_version") == _engine_version() and e.get("workload") == workload
-                and e.get("kernel") == kernel and bool(e.get("records", False)) == records):
-            return int(e["hbm_bytes_per_launch"]), e.get("source")
-    return None, None
+        return {}
+    return {e["kernel"]: e for e in (tj if isinstance(tj, list) else [tj])
+            if e.get("engine_version") == _engine_version() and e.get("workload") == workload
+            and bool(e.get("records", False)) == records}
 
 
 def main() -> int:
@@ -302,15 +304,25 @@ def main() -> int:
     total_loci = (n if args.emulate_shard else n_total) * args.steps
     value = total_loci / t_max
     ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
-    achieved = ref_bytes / (step_ms * 1e-3) / 1e9
     ev_bytes = int(work["event_bytes"]) + 12 * n   # records: 16-B result record (not 8) + 4-B row index
+    idx_bytes = int(load_stats.get("index_bytes", 0))
+    alg_bytes = idx_bytes + ev_bytes               # the engine's algorithmic bytes of one step
+    step_s = step_ms * 1e-3
+    achieved = alg_bytes / step_s / 1e9
     refine_kernel = "refine_lane_kernel" if (os.environ.get("SVTREK_GATHER", "span") != "span1" and
                                              (os.environ.get("SVTREK_LANE_W") or 2 * n >= 65536)) \
         else "refine_span_kernel"   # the engine's size-based pick (svt_engine.hip, launch)
-    traffic, traffic_src = _traffic(args.workload, "step", records=True)
-    if args.scale != 1.0 or world > 1 or args.emulate_shard:
-        traffic = traffic_src = None
-    idx_bytes = int(load_stats.get("index_bytes", 0))
+    tr = {} if (args.scale != 1.0 or world > 1 or args.emulate_shard) else _traffic(args.workload, records=True)
+    traffic = int(tr["step"]["hbm_bytes_per_launch"]) if "step" in tr else None
+    traffic_src = tr["step"].get("source") if "step" in tr else None
+    kernels = {}
+    for kname, e in tr.items():
+        if kname == "step":
+            continue
+        ns, b = e.get("avg_ns"), int(e["hbm_bytes_per_launch"])
+        kernels[kname] = {"ms": round(ns * 1e-6, 5) if ns else None, "bytes": b,
+                          "gbs": round(b / (ns * 1e-9) / 1e9, 1) if ns else None,
+                          "frac": round(b / (ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4) if ns else None}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -343,9 +355,20 @@ def main() -> int:
                        **({"emulated_shard": args.emulate_shard} if args.emulate_shard else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_over_alg": round(traffic / ref_bytes, 4) if traffic else None,
-                         "traffic_gbs": round(traffic / (step_ms * 1e-3) / 1e9, 2) if traffic else None,
+                         "frac_hbm": round(traffic / step_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                         "traffic_gbs": round(traffic / step_s / 1e9, 2) if traffic else None,
+                         "traffic_over_alg": round(traffic / alg_bytes, 4) if traffic else None,
                          "traffic_source": traffic_src,
+                         "kernels": kernels or None,
+                         "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes": "the engine's algorithmic bytes of one step: index build (svt_load_stats."
+                                      "index_bytes) + refine launch (svt_work.event_bytes + 12 B/locus records)",
+                         "reference_equivalent": {
+                             "bytes": ref_bytes, "gbs": round(ref_bytes / step_s / 1e9, 2),
+                             "frac": round(ref_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                             "def": "SURVEY 8(d): 24 B/locus + 12 B/yielded read + 4 B/CIGAR word the reference walk "
+                                    "consumes (svt_count_work); the engine walks each read once, the reference once "
+                                    "per window that yields it, so this is an effective rate, not DRAM traffic"},
                          "kernel": "step = index build (" + ", ".join(STEP_KERNELS[:2] if load_stats.get("index_kind") == 1
                                                                       else STREAM_INDEX_KERNELS) + ") + refine (" +
                                    (refine_kernel + (", refine_redo_kernel" if refine_kernel == "refine_lane_kernel"
@@ -354,23 +377,20 @@ def main() -> int:
                          "step_ms_timing": "per-step event pairs" if per_launch else
                          "one event pair around the timed steps / K",
                          "step_ms_cold": round(cold_ms, 5) if cold_ms else None,
-                         "alg_bytes_per_launch": ref_bytes,
-                         "alg_bytes": "SURVEY 8(d): 24 B/locus + 12 B/yielded read + 4 B/CIGAR word the reference "
-                                      "walk consumes (svt_count_work: windows, reads, ops_walked)",
                          "phases": {
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), per read 96 B (lane per "
-                                                "read: census soff, rec, counts; emit counts, soff, rec, offsets) or 72 B "
-                                                "(stream walk), 16 B/span event, 16 B/lead chunk unit (svt_load_stats.index_bytes)",
+                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), per read 80 B (lane per "
+                                                "read: census soff, rec, counts; emit counts, soff, rec, offsets) or 56 B "
+                                                "(stream walk), 16 B/span event (svt_load_stats.index_bytes)",
                          },
                          "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
                                           "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),
                                           "kernel": refine_kernel,
                                           "def": "the refine launch alone, priced with the span walk's own bytes: "
                                                  "36 B/locus + 32 B/query + 4 B/search entry + 16 B/span bounds + "
-                                                 "16 B/span event + 36 B/stop search + 4 B/stop chunk word (svt_work)"}},
+                                                 "16 B/span event (svt_work)"}},
             "index_build": {"index_ms_load": load_stats["index_ms"], "load_ms": load_stats,
                             "value_index_resident": round((n if args.emulate_shard else n_total) / (refine_ms * 1e-3), 1),
                             "note": "value_index_resident: loci/s of the refine launch alone, the index built once "

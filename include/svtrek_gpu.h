@@ -303,8 +303,10 @@ typedef struct svt_bgzf_block {
 svt_status svt_bgzf_inflate(svt_ctx *ctx, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
                             size_t n, uint8_t *out, size_t out_bytes);
 /* The same on device buffers (the block table on the device too; d_comp 16-B aligned and
- * readable up to 48 bytes past every block's data), asynchronous on hip_stream; svt_bgzf_inflate_status waits
- * for the stream and reports the first corrupt block (0xffffffff: none). */
+ * readable up to 48 bytes past every block's data), asynchronous on hip_stream.  Calls of one
+ * context share its scratch and error word, so they execute in submission order across streams
+ * (as every launch of the context does).  svt_bgzf_inflate_status waits for the context's last
+ * inflate (on hip_stream, ordered after it) and reports its first corrupt block (0xffffffff: none). */
 svt_status svt_bgzf_inflate_device(svt_ctx *ctx, const uint8_t *d_comp, const svt_bgzf_block *d_blocks, size_t n,
                                    uint8_t *d_out, void *hip_stream);
 svt_status svt_bgzf_inflate_status(svt_ctx *ctx, void *hip_stream, uint32_t *bad_block);

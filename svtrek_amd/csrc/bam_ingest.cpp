@@ -131,6 +131,7 @@ struct BgzfReader {
     struct Buf {
         uint8_t *p = nullptr;
         size_t cap = 0;
+        bool pinned = false;   // from inf->alloc (else malloc: pinned memory was refused)
     };
     Buf cins[2], outs[2];  // compressed input (one inflated, one being read); output (one parsed, one filled)
     size_t cin_n[2] = {0, 0};
@@ -169,20 +170,28 @@ struct BgzfReader {
     }
     void release(Buf &b) {
         if (b.p) {
-            if (inf && inf->release) inf->release(inf->user, b.p);
+            if (b.pinned) inf->release(inf->user, b.p);
             else free(b.p);
         }
         b = Buf{};
     }
-    bool reserve(Buf &b, size_t need, size_t keep) {   // grow to >= need, keeping the first `keep` bytes
+    // grow to >= need, keeping the first `keep` bytes; pinned memory when the inflater offers it,
+    // pageable memory when pinning is refused (the copies are only slower)
+    bool reserve(Buf &b, size_t need, size_t keep) {
         if (need <= b.cap) return true;
         const size_t c = std::max(need, b.cap + b.cap / 2);
-        uint8_t *q = inf && inf->alloc ? (uint8_t *)inf->alloc(inf->user, c) : (uint8_t *)malloc(c);
+        bool pinned = inf && inf->alloc && inf->release;
+        uint8_t *q = pinned ? (uint8_t *)inf->alloc(inf->user, c) : nullptr;
+        if (!q) {
+            pinned = false;
+            q = (uint8_t *)malloc(c);
+        }
         if (!q) return false;
         if (keep) memcpy(q, b.p, keep);
         release(b);
         b.p = q;
         b.cap = c;
+        b.pinned = pinned;
         return true;
     }
 
@@ -286,6 +295,11 @@ struct BgzfReader {
     Batch produce() {
         Batch b;
         Comp c = pending_comp.valid() ? pending_comp.get() : read_next();
+        // a batch of empty blocks only (ISIZE 0 each) is skipped, not taken for the end of file
+        while (c.ok && !c.blks.empty() && c.u == 0) {
+            if (eof && !carry_n) { c.blks.clear(); break; }
+            c = read_next();
+        }
         if (!c.ok) { b.err = c.err; return b; }
         if (c.blks.empty()) { b.ok = true; return b; }   // end of file
         if (!eof || carry_n) pending_comp = std::async(std::launch::async, [this] { return read_next(); });

@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_inflate.h"
 
-#define SVT_VERSION "svtrek_amd 0.16.6 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
+#define SVT_VERSION "svtrek_amd 0.17.0 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
 
 namespace {
 
@@ -52,50 +52,49 @@ constexpr uint32_t OP_INS = 1, OP_DEL = 2, OP_SOFT = 4;   // params.h:11-14
 constexpr int K_START = 0, K_END = 1, K_INS = 2;          // refine_start / refine_end / refine_ins
 constexpr int32_t T_INS = 1, T_DEL = 2;
 constexpr int BKT_SHIFT = 12;               // read-start bucket = 4096 bp
-constexpr uint32_t NCIG_MASK = 0x1fffffffu; // rec.z: n_cigar | slow << 29 | clip << 30
-constexpr uint32_t SLOW_BIT = 1u << 29;
-constexpr uint32_t STREAM_PAD = 1024;       // zero words after the CIGAR stream (index_kernel's slot over-read)
-// Lead chunks (refine_end's stop searches, refinement.c:210-221): for every read whose first op
-// is S (and that is not slow), a 16-B header {stream offset, n_cigar} and a chunk index of one
-// word per CHUNK ops -- the walk position after the chunk's last op (refinement.c:141) -- in
-// 16-B units; the read's SP_LEAD event carries its header's unit index.
-constexpr int CHUNK = 8;                    // ops per chunk
-constexpr int ALIGN_OPS = 32;               // ops per lead unit (4 chunk words = one 16-B load)
-constexpr uint32_t CH_POS = 0x1fffffffu;    // chunk word: walk position after the chunk's last op
-constexpr uint32_t LEAD_PAD = 64;           // zero words after the lead chunks
-constexpr uint64_t INDEX_LIMIT = 1ull << 29; // walks reaching position 2^29 are flagged slow
-constexpr uint64_t WALK_LIMIT = 1ull << 28;  // ... and so are walks of 2^28 bases or more (a span event's 28-bit field)
-// Span events (svt_load_pileup, index_kernel<true>): every read's breakpoint events, 16 B each,
+constexpr uint32_t NCIG_MASK = 0x1fffffffu; // rec.z: n_cigar | clip << 30
+constexpr uint32_t STREAM_PAD = 4096;       // zero words after the CIGAR stream (the index walks' slot over-read)
+// Walk positions in the index saturate at IX_SAT.  The reference's uint32 reference_pos
+// (refinement.c:118-145) cannot wrap before it passes a window end below 2^30 (one op
+// advances it by < 2^28), so for every window with e < WEXACT "walk position <= e" and every
+// candidate value are exact on saturated positions; windows ending at or past WEXACT take the
+// per-read replay of the reference's uint32 arithmetic (walk_read).
+constexpr uint32_t IX_SAT = 1u << 30;
+constexpr uint32_t WEXACT = 1u << 30;
+// Span events (svt_load_pileup, the index builds): every read's breakpoint events, 16 B each,
 // self-contained {x, w, endpos, aux} so that a window is one filter over a contiguous span:
-//   D list: SP_LEAD {pos, walk << 4 | SP_LEAD, endpos, lead unit} for cigar[0] == S (:210),
-//           D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:188),
-//           SP_TRAIL {walk end, SP_TRAIL, endpos, 0} for cigar[n-1] == S (:120,:147);
+//   D list: D > 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:124,:188),
+//           SP_TRAIL {walk end, SP_TRAIL, endpos, 0} for cigar[n-1] == S (:120,:147),
+//           SP_LEAD {pos, SP_LEAD, endpos, walk end} for cigar[0] == S (:210);
 //   I list: I >= 50 ops {walk position before the op, CIGAR word, endpos, 0} (refinement.c:299).
 constexpr uint32_t SP_TRAIL = 0xEu, SP_LEAD = 0xFu;   // op codes no candidate event carries
 
 struct DevPileup {
     const int32_t *pos;       // [n_reads]
     const int32_t *emax;      // [n_reads] prefix max of endpos within the contig
-    const uint4 *rec;         // [n_reads] {pos, endpos, n_cig | slow<<29 | clip<<30, 0}
+    const uint4 *rec;         // [n_reads] {pos, endpos, n_cig | clip<<30, 0}
     const uint64_t *off64;    // [n_reads+1] read r's CIGAR = cigar[off64[r] .. off64[r] + n_cig)
     const int64_t *tid_off;   // [n_targets+1]
     const int64_t *bkt_off;   // [n_targets+1] start of each contig's bucket table
     const uint2 *bkt;         // {first read with pos >= b << BKT_SHIFT, first read with emax >= b << BKT_SHIFT}
     const uint32_t *cigar;    // the CIGAR stream (caller's words; one 0M word for n_cigar == 0 reads)
-    const uint32_t *lchunk;   // lead chunks: per leading-S read a 16-B header {stream offset, n_cigar}
-                              // and its chunk index (the walk position after every CHUNK ops, CH_POS)
-    const uint64_t *insbase;  // [n_reads+1] I >= 50 ops before read r (every read)
     const uint64_t *spoffD;   // [n_reads+1] span events: read r's D-list events are spD[spoffD[r] .. spoffD[r+1])
     const uint64_t *spoffI;   // [n_reads+1]              its I-list events spI[spoffI[r] .. spoffI[r+1])
+                              // (= the I >= 50 ops before read r: the POA mode's sequence index)
     const uint4 *spD;
     const uint4 *spI;
-    const uint64_t *slowpre;  // [n_reads+1] slow reads before read r (their walks take walk_read)
     int32_t n_targets;
 };
 
 struct KParams {
     int32_t wider, median, narrow, range, ci, min_count;
     int32_t sw_window, sw_slide;   // sliding_window_ins mode only
+    // refine_end's leading-S reads whose walk passes e (refinement.c:210-221) push the position
+    // after the break op + 1 >= e + 2.  When e + 2 already lies at or past everything the vote
+    // reads -- pos + range + max(ci, 0) and pos + 26 (narrow + 2 >= both widths) -- any value
+    // >= e + 2 votes the same (see band_filter), so these reads count as one candidate at e + 2
+    // and no stop search is needed; otherwise refine_end windows take the per-read replay.
+    int32_t sent_ok;
 };
 
 struct KArgs {
@@ -126,7 +125,6 @@ constexpr int W_WINDOWS = 0, W_READS = 1, W_OPS = 2, W_CANDS = 3, W_SPILLED = 4,
               W_SPAN = 13, W_N = 14;
 constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status, work counters
 constexpr size_t CTL_REDO = 200;    // two redo counters (alternating launches)
-constexpr size_t CTL_XCNT = 208;    // ranges listed for the exact index census
 static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
 
 // ------------------------------------------------------------------ wave primitives
@@ -381,112 +379,6 @@ __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141:
 #endif
 
 
-// A lead read's CIGAR in the stream: its header's offset (lead unit u).
-__device__ __forceinline__ uint64_t lead_soff(const DevPileup &P, uint64_t u) {
-    const uint2 h = *reinterpret_cast<const uint2 *>(P.lchunk + u * 4u);
-    return (uint64_t)h.x | (uint64_t)h.y << 32;
-}
-
-// Walk position after the break op of a leading-S read that breaks (walk end > e): the first
-// op whose walk position after it exceeds e, from the read's lead chunks (first unit u).
-// Wave-cooperative, uniform arguments; `op_idx` receives the break op's index in the read.
-__device__ __forceinline__ uint32_t break_after(const DevPileup &P, uint64_t u, uint32_t ncig, uint32_t rpos,
-                                                uint32_t e, uint32_t &op_idx) {
-    const int ln = lane_id();
-    const uint64_t c0 = (u + 1u) * 4u;
-    const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
-    uint32_t bc = nch, before = rpos;   // break chunk, walk position before it
-    for (uint32_t b = 0; b < nch; b += 4 * WAVE) {
-        const uint32_t c = b + 4u * (uint32_t)ln;
-        const uint4 q = c < nch ? *reinterpret_cast<const uint4 *>(P.lchunk + c0 + c) : make_uint4(0, 0, 0, 0);
-        const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
-        uint32_t first = 4;
-#pragma unroll
-        for (int i = 3; i >= 0; i--)
-            if (c + (uint32_t)i < nch && E[i] > e) first = (uint32_t)i;
-        const uint64_t m = ballot(first < 4);
-        if (m) {
-            const int l = __builtin_ctzll(m);
-            const uint32_t f = rdlane(first, l);
-            bc = b + 4u * (uint32_t)l + f;
-            // walk position before chunk bc: the previous chunk's end (same or previous lane)
-            const uint32_t prev = f == 0 ? 0u : f == 1 ? E[0] : f == 2 ? E[1] : E[2];
-            const uint32_t prev_lane = dpp<0x138, 0xf>(E[3]);   // wave_shr:1
-            const uint32_t pv = rdlane(f ? prev : prev_lane, l);
-            before = bc == 0 ? rpos : (f == 0 && l == 0 ? before : pv);
-            break;
-        }
-        before = rdlane(E[3], WAVE - 1);   // chunk b + 4*64 - 1 ends here (all <= e)
-    }
-    // the break op inside chunk bc: lanes 0-7 take its ops
-    const uint32_t w = ln < CHUNK ? P.cigar[lead_soff(P, u) + (uint64_t)bc * CHUNK + (uint32_t)ln] : 0u;
-    const uint32_t after = before + wave_scan_add(ln < CHUNK ? ref_adv(w) : 0u);
-    const uint64_t m = ballot(ln < CHUNK && after > e);
-    const int k = __builtin_ctzll(m);   // exists: the chunk ends past e
-    op_idx = bc * CHUNK + (uint32_t)k;
-    return rdlane(after, k);
-}
-
-// Row-parallel form of break_after for refine_end's soft-clip stops: up to 4 breaking reads
-// at once, one 16-lane row each (DPP row shifts never cross a row).  Lanes of row g take
-// read `l` = the g-th set bit of `m` (block lane), consume those bits, and push after + 1.
-// The read's lead arena block comes with its SP_LEAD event (blk_v), so no per-read load is on
-// this path.
-__device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t m, uint32_t ncig_v, uint32_t rpos_v,
-                                              uint32_t blk_v, uint32_t e, Sink &sink) {
-    const int ln = lane_id(), g = ln >> 4, t = ln & 15;
-    int my = -1;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        if (!m) break;
-        const int l = __builtin_ctzll(m);
-        m &= m - 1;
-        if (g == q) my = l;
-    }
-    const bool has = my >= 0;
-    // per-row read parameters (a bpermute from the read's block lane)
-    const uint32_t ncig = (uint32_t)__shfl((int)ncig_v, has ? my : 0, WAVE);
-    const uint32_t rpos = (uint32_t)__shfl((int)rpos_v, has ? my : 0, WAVE);
-    const uint32_t blk = (uint32_t)__shfl((int)blk_v, has ? my : 0, WAVE);
-    const uint64_t c0 = ((uint64_t)blk + 1u) * 4u;   // the read's chunk words (after its header)
-    const uint32_t nch = (ncig + CHUNK - 1) / CHUNK;
-    bool found = false;
-    uint32_t bc = 0;
-    for (uint32_t it = 0;; it += 64) {   // 64 chunks (16 lanes x 4) per row per step
-        const uint32_t c = it + 4u * (uint32_t)t;
-        const bool act = has && !found && c < nch;
-        const uint4 q = act ? *reinterpret_cast<const uint4 *>(P.lchunk + c0 + c) : make_uint4(0, 0, 0, 0);
-        const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
-        uint32_t first = 4;
-#pragma unroll
-        for (int i = 3; i >= 0; i--)
-            if (act && c + (uint32_t)i < nch && E[i] > e) first = (uint32_t)i;
-        const uint32_t rm = (uint32_t)(ballot(first < 4) >> (16 * g)) & 0xffffu;
-        const int lr = rm ? __builtin_ctz(rm) : 0;
-        const uint32_t f = (uint32_t)__shfl((int)first, 16 * g + lr, WAVE);
-        if (has && !found && rm) {
-            bc = it + 4u * (uint32_t)lr + f;
-            found = true;
-        }
-        if (!ballot(has && !found && it + 64 < nch)) break;
-    }
-    // the break chunk's ops (row lanes 0-7) and the walk position before it (row lane 8)
-    const uint32_t w = has && t < CHUNK ? P.cigar[lead_soff(P, blk) + (uint64_t)bc * CHUNK + (uint32_t)t] : 0u;
-    const uint32_t pv = has && t == CHUNK ? (bc ? P.lchunk[c0 + bc - 1] & CH_POS : rpos) : 0u;
-    const uint32_t before = (uint32_t)__shfl((int)pv, 16 * g + CHUNK, WAVE);
-    uint32_t x = t < CHUNK ? ref_adv(w) : 0u;
-    x += dpp<0x111, 0xf>(x);   // inclusive row scan
-    x += dpp<0x112, 0xf>(x);
-    x += dpp<0x114, 0xf>(x);
-    x += dpp<0x118, 0xf>(x);
-    const uint32_t after = before + x;
-    const uint32_t bm = (uint32_t)(ballot(t < CHUNK && after > e) >> (16 * g)) & 0xffu;   // break op exists
-    const uint32_t a = (uint32_t)__shfl((int)after, 16 * g + (bm ? __builtin_ctz(bm) : 0), WAVE);
-    if (has && t == 0) sink.push1((int32_t)(a + 1u));   // refinement.c:210-220
-    return m;
-}
-
-
 // ------------------------------------------------------------------ span walk (default)
 // The reads [lo, hi) of a window own one contiguous span of the D (or I) event list, and
 // every event carries what its tests need (its read's endpos for the overlap test of
@@ -495,51 +387,32 @@ __device__ __forceinline__ uint64_t stop_rows(const DevPileup &P, uint64_t m, ui
 // An op is processed by the reference walk iff the walk position before it is <= inter.end
 // (positions only grow along a read, refinement.c:145), so a candidate event counts iff
 // x <= e; the soft-clip events follow refinement.c:147-159 (trailing S: no break, s <= walk
-// end <= e) and :210-220 (leading S, s <= pos <= e: walk end + 1, or the position after the
-// break op + 1 -- found by stop_rows in the chunk index).
+// end <= e) and :210-220 (leading S, s <= pos <= e: walk end + 1, or -- the walk passes e --
+// the position after the break op + 1, which votes as e + 2: KParams::sent_ok).
 constexpr int SPAN_U = 4;   // 16-B event loads in flight per lane
 
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// The span walk's own reads, for svt_count_work: the two span bounds, the events of the
-// span, and per leading-S stop the chunk words scanned to the break chunk.
+// The span walk's own reads, for svt_count_work: the region query and the events of the span.
 template <int KIND>
 __device__ __forceinline__ void span_count(const DevPileup &P, int tid, uint32_t s, uint32_t e, WinStats &st) {
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
     int64_t lo, hi;
     if (!read_range(P, tid, beg, end, lo, hi, &st)) return;
     const uint64_t *off = KIND == K_INS ? P.spoffI : P.spoffD;
-    const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
-    const uint64_t E0 = off[lo], E1 = off[hi];
     st.squeries++;
-    st.span += E1 - E0;
-    if (KIND != K_END) return;
-    for (uint64_t b = E0; b < E1; b += WAVE) {
-        const uint64_t j = b + (uint64_t)lane_id();
-        const uint4 v = j < E1 ? ev[j] : make_uint4(0, 0, 0, 0);
-        const bool brk = (v.y & 0xfu) == SP_LEAD && (int64_t)(int32_t)v.z > beg && s <= v.x && v.x <= e &&
-                         v.x + (v.y >> 4) > e;
-        uint64_t m = ballot(brk);
-        while (m) {
-            const int l = __builtin_ctzll(m);
-            m &= m - 1;
-            uint32_t bi;
-            (void)break_after(P, (uint64_t)rdlane(v.w, l), NCIG_MASK, rdlane(v.x, l), e, bi);
-            st.stops++;
-            st.stopch += (unsigned long long)(bi / CHUNK + 1u);
-        }
-    }
+    st.span += off[hi] - off[lo];
 }
 
 // read_range (A3) with the span bounds read in the same dependent step as the pos/emax
-// probes: each probe lane also loads the span offset and slow-read prefix of its read, and
-// the bounds are taken from the lanes where the two searches end (one HBM round trip less
-// per window).  Wider bucket ranges fall back to read_range + one more step.
+// probes: each probe lane also loads the span offset of its read, and the bounds are taken
+// from the lanes where the two searches end (one HBM round trip less per window).  Wider
+// bucket ranges fall back to read_range + one more step.
 template <int KIND>
-__device__ __forceinline__ bool span_query(const DevPileup &P, int tid, int64_t beg, int64_t end, int64_t &lo,
-                                           int64_t &hi, uint64_t &E0, uint64_t &E1, uint64_t &nslow) {
+__device__ __forceinline__ bool span_query(const DevPileup &P, int tid, int64_t beg, int64_t end, uint64_t &E0,
+                                           uint64_t &E1) {
     if (tid < 0 || tid >= P.n_targets || end <= beg) return false;   // no reads (A3)
     const int64_t ra = P.tid_off[tid], nr = P.tid_off[tid + 1] - ra;
     if (nr == 0) return false;
@@ -550,11 +423,11 @@ __device__ __forceinline__ bool span_query(const DevPileup &P, int tid, int64_t 
     const uint2 bw = ln < 4 ? P.bkt[b0 + bi] : make_uint2(0, 0);
     const int64_t hl = rdlane(bw.x, 0), hh = rdlane(bw.x, 1), ll = rdlane(bw.y, 2), lh = rdlane(bw.y, 3);
     if (hh - hl >= WAVE || lh - ll >= WAVE) {   // wide bucket: the general search, then the bounds
+        int64_t lo, hi;
         if (!read_range(P, tid, beg, end, lo, hi)) return false;
-        const uint64_t ob = ln < 2 ? off[ln ? hi : lo] : ln < 4 ? P.slowpre[ln == 3 ? hi : lo] : 0ull;
+        const uint64_t ob = ln < 2 ? off[ln ? hi : lo] : 0ull;
         E0 = rdlane64(ob, 0);
         E1 = rdlane64(ob, 1);
-        nslow = rdlane64(ob, 3) - rdlane64(ob, 2);
         return true;
     }
     // lanes [0, hh-hl] cover the hi candidates hl .. hh, lanes [0, lh-ll] the lo candidates
@@ -562,65 +435,33 @@ __device__ __forceinline__ bool span_query(const DevPileup &P, int tid, int64_t 
     const int64_t rh = ra + (vh ? hl + ln : hl), rl = ra + (vl ? ll + ln : ll);
     const int32_t pv = vh && hl + ln < hh ? P.pos[rh] : 0, ev = vl && ll + ln < lh ? P.emax[rl] : 0;
     const uint64_t oh = off[rh], ol = off[rl];
-    const uint64_t sh = P.slowpre[rh], sl = P.slowpre[rl];
     const uint64_t mh = ballot(vh && hl + ln < hh && (int64_t)pv >= end);
     const uint64_t ml = ballot(vl && ll + ln < lh && (int64_t)ev > beg);
     const int kh = mh ? __builtin_ctzll(mh) : (int)(hh - hl), kl = ml ? __builtin_ctzll(ml) : (int)(lh - ll);
-    hi = ra + hl + kh;
-    lo = ra + ll + kl;
-    if (lo >= hi) return false;
+    if (ll + kl >= hl + kh) return false;
     E1 = rdlane64(oh, kh);
     E0 = rdlane64(ol, kl);
-    nslow = rdlane64(sh, kh) - rdlane64(sl, kl);
     return true;
 }
 
-// The span walk proper: events [E0, E1) of the yielded reads [lo, hi) of window [s, e]
-// (query beg = s-1), nslow = the slow reads among them.  Leaves the candidate count in
-// *sink.cnt.
-// A refine_end stop search deferred by the lane kernel: the breaking read's arena offset / 32,
-// its pos, the window end, the window (searched later for a whole chunk of windows at once).
-struct StopReq {
-    uint32_t op32, rpos, e, kw;   // the read's lead unit, its pos, the window end, the window
-};
-struct StopList {
-    StopReq *q;
-    int32_t *cnt;   // LDS counter (may exceed cap: the window then takes the wave-wide path)
-    int32_t cap;
-    uint32_t kw;
-};
-// The lane kernel's queue: the count is wave-uniform and only this wave appends, so it lives
-// in a scalar register (may exceed LV_STOPS: those windows take the wave-wide path).
-struct LaneStops {
-    StopReq *q;
-    int32_t n;
-    uint32_t kw;
-};
-
-// One span event's test for window [s, e] (query beg = s-1): c = it is a candidate with value
-// val; brk = a leading-S read whose walk passes e (refine_end's stop search, :210-221).
+// One span event's test for window [s, e] (query beg = s-1): it is a candidate with value val.
+// A leading-S read whose walk passes e (refine_end's stop, :210-221) is one at e + 2.
 template <int KIND>
-__device__ __forceinline__ bool span_cand(const uint4 &v, uint32_t s, uint32_t e, int32_t beg32, uint32_t &val,
-                                          bool &brk) {
+__device__ __forceinline__ bool span_cand(const uint4 &v, uint32_t s, uint32_t e, int32_t beg32, uint32_t &val) {
     const uint32_t x = v.x, op = v.y & 0xfu, len = v.y >> 4;
     const bool ovl = (int32_t)v.z > beg32;   // hts_itr_next overlap; pos < end holds below hi
-    brk = false;
     val = x;
     if (KIND == K_INS) return ovl && op == OP_INS && x <= e;                   // refinement.c:299
     if (KIND == K_START) return ovl && x <= e && (op == OP_DEL || (op == SP_TRAIL && s <= x));   // :124 / :147-159
     const bool lead = op == SP_LEAD && ovl && s <= x && x <= e;                // :210-220
-    const uint32_t wend = x + len;
-    brk = lead && wend > e;
-    val = op == OP_DEL ? x + len + 1u : wend + 1u;
-    return (ovl && x <= e && op == OP_DEL) || (lead && !brk);                  // :188-199
+    val = op == OP_DEL ? x + len + 1u : v.w > e ? e + 2u : v.w + 1u;
+    return (ovl && x <= e && op == OP_DEL) || lead;                            // :188-199
 }
 
 template <int KIND>
-__device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t s, uint32_t e, int64_t lo, int64_t hi,
-                                          uint64_t E0, uint64_t E1, uint64_t nslow, Sink &sink,
-                                          const StopList *defer = nullptr) {
-    const int64_t beg = (int64_t)(uint32_t)(s - 1u);
-    const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);   // read_range yielded reads: beg < end <= 2^31 - 1
+__device__ __forceinline__ void span_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint64_t E1,
+                                          Sink &sink) {
+    const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);   // yielded reads: beg < end <= 2^30
     const int ln = lane_id();
     const uint4 *ev = KIND == K_INS ? P.spI : P.spD;
     int32_t cnt = 0;   // candidates appended so far (wave-uniform)
@@ -638,71 +479,36 @@ __device__ __forceinline__ void span_walk(const DevPileup &P, int tid, uint32_t 
         for (int u = 0; u < SPAN_U; u++) {
             if ((uint64_t)(u * WAVE) >= left) break;
             if ((uint64_t)(u * WAVE + ln) >= left) v[u] = make_uint4(0, 0, 0, 0);   // zero event: no candidate
-            const uint32_t x = v[u].x;
-            bool brk;
             uint32_t val;
-            const bool c = span_cand<KIND>(v[u], s, e, beg32, val, brk);
+            const bool c = span_cand<KIND>(v[u], s, e, beg32, val);
             const uint64_t m = ballot(c);
             const int32_t idx = cnt + (int32_t)mbcnt(m);
             if (c && idx < sink.cap) sink.buf[idx] = (int32_t)val;
             cnt += (int32_t)__popcll(m);
-            if (KIND == K_END && SVT_DIAG != 3) {
-                uint64_t sm = ballot(brk);
-                if (sm && defer) {   // queued: the lane kernel searches a whole chunk's reads at once
-                    int32_t base = 0;
-                    if (ln == 0) base = atomicAdd(defer->cnt, (int32_t)__popcll(sm));
-                    base = rdlane_i(base, 0);
-                    const int32_t qi = base + (int32_t)mbcnt(sm);
-                    if (brk && qi < defer->cap) {
-                        defer->q[qi] = StopReq{v[u].w, x, e, defer->kw};
-                    }
-                } else if (sm) {   // the position after the break op, rare: the sink's LDS counter takes over
-                    if (ln == 0) *sink.cnt = cnt;
-                    wave_sync();
-                    while (sm) sm = stop_rows(P, sm, NCIG_MASK, x, v[u].w, e, sink);
-                    wave_sync();
-                    cnt = uniform_i(*sink.cnt);
-                }
-            }
         }
     }
     if (ln == 0) *sink.cnt = cnt;
-    if (nslow) {   // reads whose walk could leave the event range: exact per-read replay (never in practice)
-        WinStats st;
-        wave_sync();
-        for (int64_t rb = lo; rb < hi; rb += WAVE) {
-            const int64_t r = rb + ln;
-            const uint4 rc = r < hi ? P.rec[r] : make_uint4(0, 0, 0, 0);
-            uint64_t sm = ballot((rc.z & SLOW_BIT) && (int64_t)(int32_t)rc.y > beg);
-            while (sm) {
-                const int l = __builtin_ctzll(sm);
-                sm &= sm - 1;
-                const uint32_t z = rdlane(rc.z, l);
-                walk_read<KIND, false>(P.cigar, P.off64[rb + l], z & NCIG_MASK, rdlane(rc.x, l), z >> 30, s, e, sink, st);
-            }
-        }
-    }
 }
 
+// The wave-wide gather of one window: the span walk, or the reference's own per-read walk for
+// windows ending at or past WEXACT and for refine_end windows whose leading-S stops cannot
+// vote as e + 2 (!sent_ok).
 template <int KIND, bool COUNT>
-__device__ __forceinline__ void gather_span(const DevPileup &P, int tid, uint32_t s, uint32_t e, Sink &sink,
-                                            WinStats &st) {
+__device__ __forceinline__ void gather_span(const DevPileup &P, const KParams &k, int tid, uint32_t s, uint32_t e,
+                                            Sink &sink, WinStats &st) {
     if (COUNT) {   // diagnostic: the reference's work by the exact per-read walk + what the span walk reads
         gather_perread<KIND, true>(P, tid, s, e, sink, st);
-        if (e < 0x80000000u) span_count<KIND>(P, tid, s, e, st);
+        if (e < WEXACT) span_count<KIND>(P, tid, s, e, st);
         return;
     }
-    // Event positions are walk positions < 2^29 (longer walks are flagged slow at load time
-    // and carry no events); windows ending at or past 2^31 take the exact per-read path.
-    if (e >= 0x80000000u) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
+    if (e >= WEXACT || (KIND == K_END && !k.sent_ok)) { gather_perread<KIND, COUNT>(P, tid, s, e, sink, st); return; }
     const int64_t beg = (int64_t)(uint32_t)(s - 1u), end = (int64_t)(uint32_t)(e - 1u);
-    int64_t lo, hi;
-    uint64_t E0, E1, nslow;
-    if (!span_query<KIND>(P, tid, beg, end, lo, hi, E0, E1, nslow)) return;
+    uint64_t E0, E1;
+    if (!span_query<KIND>(P, tid, beg, end, E0, E1)) return;
 #if SVT_DIAG == 1
-    if (lo < hi) return;     // diagnostic build: region query only
+    return;     // diagnostic build: region query only
 #endif
-    span_walk<KIND>(P, tid, s, e, lo, hi, E0, E1, nslow, sink);
+    span_walk<KIND>(P, s, e, E0, E1, sink);
 }
 
 // ------------------------------------------------------------------ sort + vote (A8-A10)
@@ -1178,7 +984,7 @@ __device__ __forceinline__ int32_t gather(const KArgs &a, int tid, uint32_t s, u
     wave_sync();
     static_assert(G == G_SPAN, "span walk only");
     (void)L;
-    gather_span<KIND, COUNT>(a.pile, tid, s, e, sink, st);
+    gather_span<KIND, COUNT>(a.pile, a.prm, tid, s, e, sink, st);
     wave_sync();
     return uniform_i(*sink.cnt);
 }
@@ -1419,7 +1225,6 @@ struct LvMeta {
     uint32_t flags;   // nb | LV_* bits
     int32_t n;        // candidates (min_count test)
 };
-constexpr int LV_STOPS = 64;   // deferred stop searches per chunk
 constexpr uint32_t LV_NONE = 1u << 14;   // no window (INV / other types): NA
 // diagnostic build 11: why a window left the lane path (bits 16+), reported as its result
 #if SVT_DIAG == 11
@@ -1432,7 +1237,6 @@ template <int W>
 struct LaneLds {
     uint16_t stage[W * LV_S];   // parked queries (phase 0 -> 1), band offsets (1 -> 2)
     LvMeta meta[W];
-    StopReq stops[LV_STOPS];
 };
 
 // Phase 1 of one window, wave-wide (A4-A7 + the band): the window's span events [E0, E0+len)
@@ -1443,7 +1247,8 @@ struct LaneLds {
 // an OR-ed lane mask (with the band they give the whole-multiset facts, lane_vote).  Values are
 // walk positions < 2^29 + 1 (reads reaching 2^28 bases or position 2^29 are slow and carry
 // no events), so every candidate is >= 0 and within +-2^30: no int64 path is ever needed.
-// refine_end's breaking leading-S reads are queued for phase 1b (stop_lane).
+// refine_end's leading-S reads whose walk passes e count as one candidate at or above the
+// band's high end (KParams::sent_ok).
 struct LaneBand {
     int32_t n;        // candidates collected (before the stop searches)
     int32_t nb;       // band members (> LV_CAP: the row overflowed)
@@ -1452,8 +1257,8 @@ struct LaneBand {
 
 // span_cand as lane masks, one compare per ballot (each folds into one v_cmp writing an SGPR
 // pair; the conditions are combined on the scalar unit).  refine_end's value is x + len + 1
-// for both of its candidate kinds (D: the position after the op + 1; leading S that does not
-// break: walk end + 1).
+// for a D op and walk end + 1 for a leading S that does not break; brk: a leading S whose walk
+// passes e (a candidate at e + 2 >= the band's high end).
 template <int KIND>
 __device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, uint32_t e, int32_t beg32,
                                                    uint64_t &brk) {
@@ -1463,7 +1268,7 @@ __device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, u
     if (KIND == K_INS) return ovl & le & ballot(op == OP_INS);                                  // refinement.c:299
     if (KIND == K_START) return ovl & le & (ballot(op == OP_DEL) | (ballot(op == SP_TRAIL) & ballot(s <= x)));
     const uint64_t lead = ovl & le & ballot(op == SP_LEAD) & ballot(s <= x);                    // :210-220
-    brk = lead & ballot(x + (v.y >> 4) > e);
+    brk = lead & ballot(v.w > e);
     return (ovl & le & ballot(op == OP_DEL)) | (lead & ~brk);                                   // :188-199
 }
 
@@ -1474,8 +1279,7 @@ constexpr int LW_U = SVT_LW_U;   // 64-event slots per step of lane_walk (loads 
 
 template <int KIND>
 __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
-                                              int32_t lo, int32_t hi, uint16_t *row,
-                                              LaneStops &defer) {
+                                              int32_t lo, int32_t hi, uint16_t *row) {
     const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);
     const int ln = lane_id();
     const uint4 *ev = (KIND == K_INS ? P.spI : P.spD) + E0;   // wave-uniform base: 32-bit lane offsets
@@ -1498,8 +1302,11 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
                 cm &= in;
                 brk &= in;
             }
-            const int32_t iv = (int32_t)(KIND == K_END ? v[u].x + (v[u].y >> 4) + 1u : v[u].x);
-            n += (int32_t)__popcll(cm);
+            const int32_t iv = (int32_t)(KIND == K_END ? ((v[u].y & 0xfu) == OP_DEL ? v[u].x + (v[u].y >> 4) + 1u
+                                                                                   : v[u].w + 1u)
+                                                       : v[u].x);
+            n += (int32_t)__popcll(cm | brk);
+            above |= brk;
             const uint64_t gt = ballot(iv > lo), lt = ballot(iv < hi);
             below |= cm & ~gt;
             above |= cm & ~lt;
@@ -1507,15 +1314,6 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
             // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone)
             if (__builtin_amdgcn_inverse_ballot_w64(mb)) row[min(nb + (int32_t)mbcnt(mb), LV_CAP)] = (uint16_t)(iv - lo);
             nb += (int32_t)__popcll(mb);
-            if (KIND == K_END && SVT_DIAG != 3) {
-                if (brk) {   // queued: searched for the whole chunk of windows at once (phase 1b)
-                    const int32_t qi = defer.n + (int32_t)mbcnt(brk);
-                    defer.n += (int32_t)__popcll(brk);
-                    if (__builtin_amdgcn_inverse_ballot_w64(brk) && qi < LV_STOPS) {
-                        defer.q[qi] = StopReq{v[u].w, v[u].x, e, defer.kw};
-                    }
-                }
-            }
         }
     }
     return LaneBand{n, nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
@@ -1631,45 +1429,9 @@ __device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &l
 #define SVT_LANE_VOTE 1
 #endif
 
-// One deferred stop search, per lane (refinement.c:210-221 for a read that breaks): the
-// position after the op whose walk end first passes e.  The chunk index holds the walk
-// position after every 8 arena ops; the read's chunks are scanned 4 at a time (its first
-// chunk is 4-chunk aligned: reads start on 32-op boundaries), then the break chunk's 8 ops.
-__device__ __forceinline__ uint32_t stop_lane(const DevPileup &P, const StopReq &r) {
-    const uint64_t c0 = ((uint64_t)r.op32 + 1u) * 4u;      // the read's chunk words (after its header)
-    const uint64_t so = lead_soff(P, r.op32);               // its CIGAR in the stream (loaded alongside)
-    uint32_t prev = r.rpos, bc = 0, before = r.rpos;
-    for (uint32_t c = 0;; c += 4) {   // the break exists (walk end > e): the scan ends inside the read
-        const uint4 q = *reinterpret_cast<const uint4 *>(P.lchunk + c0 + c);
-        const uint32_t E[4] = {q.x & CH_POS, q.y & CH_POS, q.z & CH_POS, q.w & CH_POS};
-        int f = 4;
-#pragma unroll
-        for (int i = 3; i >= 0; i--)
-            if (E[i] > r.e) f = i;
-        if (f < 4) {
-            bc = c + (uint32_t)f;
-            before = f == 0 ? prev : E[f - 1];
-            break;
-        }
-        prev = E[3];
-    }
-    const uint32_t *cw = P.cigar + so + (uint64_t)bc * CHUNK;   // the break chunk's ops (any alignment)
-    uint32_t W[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) W[i] = cw[i];
-    uint32_t after = before, res = 0;
-    bool found = false;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        after += ref_adv(W[i]);
-        if (!found && after > r.e) { res = after; found = true; }
-    }
-    return res + 1u;   // refinement.c:220
-}
-
 // One window's A2 + A3 answer, computed by one lane (phase 0).  u32 words only (the rows
 // it is parked in are 4-byte aligned).
-constexpr int32_t LQ_REDO = 1 << 4;   // kind bit: the window takes the wave-wide path (slow reads / e >= 2^31)
+constexpr int32_t LQ_REDO = 1 << 4;   // kind bit: the window takes the wave-wide path
 struct LvQuery {
     int32_t kind;          // K_* (| LQ_REDO), -1: no window (NA)
     int32_t lo;            // the vote's band low end: pos - (range + max(ci, 0))
@@ -1692,10 +1454,14 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
     else if (L.type == T_DEL) { q.kind = K_END; q.s = end - (uint32_t)k.narrow; q.e = end + (uint32_t)k.narrow; imp = end; }
     // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250): NA, NA
     if (q.kind < 0) return;
-    // the exact per-read path (gather_span) for windows ending at or past 2^31; the wave-wide
-    // vote when the band is off (band_ok) or pos is beyond +-2^30 (int32 differences could wrap)
+    // the wave-wide path (refine_redo_kernel) when the window ends at or past WEXACT or is a
+    // refine_end window whose stops need the per-read replay (gather_span), when the band is off
+    // (band_ok) or pos is beyond +-2^30 (int32 differences could wrap)
     constexpr int32_t LIM = 1 << 30;
-    if (q.e >= 0x80000000u || !band_ok || (int32_t)imp <= -LIM || (int32_t)imp >= LIM) { q.kind |= LQ_REDO; return; }
+    if (q.e >= WEXACT || (q.kind == K_END && !k.sent_ok) || !band_ok || (int32_t)imp <= -LIM || (int32_t)imp >= LIM) {
+        q.kind |= LQ_REDO;
+        return;
+    }
     q.lo = (int32_t)imp - (k.range + max(k.ci, 0));
     q.len = 0;   // empty span: no reads
     const int tid = L.chrom - 1;
@@ -1720,8 +1486,8 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
     if (lo >= hi) return;
     const uint64_t *off = q.kind == K_INS ? P.spoffI : P.spoffD;
     const uint64_t E0 = off[lo], E1 = off[hi];
-    // slow reads: exact per-read replay; spans of 2^31 events or more: the wave-wide path
-    if (P.slowpre[hi] != P.slowpre[lo] || E1 - E0 >= 0x80000000ull) { q.kind |= LQ_REDO; return; }
+    // spans of 2^31 events or more: the wave-wide path
+    if (E1 - E0 >= 0x80000000ull) { q.kind |= LQ_REDO; return; }
     q.e0[0] = (uint32_t)E0; q.e0[1] = (uint32_t)(E0 >> 32);
     q.len = (uint32_t)(E1 - E0);
 }
@@ -1758,7 +1524,6 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         return;
     }
     // ---- phase 1: span walk + band per window (wave-wide)
-    LaneStops stops{L.stops, 0, 0u};   // refine_end's deferred stop searches (phase 1b)
     for (uint32_t kw = 0; kw < cnt; kw++) {
         const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.stage + kw * LV_S);
         const int32_t qk = uniform_i(qp->kind);
@@ -1773,50 +1538,21 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         if (qk < 0) {
             flags = LV_NONE;
         } else if (qk & LQ_REDO) {
-            flags = LV_REDO | LV_WHY(1);   // slow reads, a window past 2^31, the band off
+            flags = LV_REDO | LV_WHY(1);   // a window past WEXACT, per-read stops, the band off
         } else {
-            const int32_t ns0 = stops.n;
-            stops.kw = kw;
             LaneBand r{0, 0, 0u};
             uint16_t *row = L.stage + kw * LV_S;
             if (len) {
-                if (qk == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, stops);
-                else if (qk == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, stops);
-                else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row, stops);
+                if (qk == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row);
+                else if (qk == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row);
+                else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row);
             }
-            flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : stops.n > LV_STOPS ? LV_REDO | LV_WHY(4)
-                                                                            : (uint32_t)r.nb | LV_PENDING | r.flags;
-            n = r.n + stops.n - ns0;   // the deferred stop candidates count toward min_count
+            flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : (uint32_t)r.nb | LV_PENDING | r.flags;
+            n = r.n;
         }
         if (ln == 0) {
             L.meta[kw].flags = flags;
             L.meta[kw].n = n;
-        }
-        wave_sync();
-    }
-    // ---- phase 1b: the chunk's deferred stop searches, one lane each, folded into their
-    // windows' bands (counts by LDS atomics; band members appended to the staging rows)
-    {
-        const int32_t nsq = min(stops.n, LV_STOPS);
-        if (ln < nsq) {
-            const StopReq rq = L.stops[ln];
-            const int32_t v = (int32_t)stop_lane(a.pile, rq);
-            LvMeta &m = L.meta[rq.kw];
-            const uint32_t fl = m.flags;
-            if (fl & LV_PENDING) {
-                constexpr int32_t LIM = 1 << 30;
-                const int32_t lo = m.lo, hi = lo + 2 * bw;
-                uint32_t set = 0;
-                if (v <= lo) set |= LV_BELOW;
-                if (v >= hi) set |= LV_ABOVE;
-                if (v <= -LIM || v >= LIM || (lo < v && v < hi && v < 0)) set |= LV_REDO | LV_WHY(5);
-                if (set) atomicOr(&m.flags, set);
-                if (lo < v && v < hi) {
-                    const uint32_t idx = atomicAdd(&m.flags, 1u) & 0xffu;   // nb is the low byte
-                    if (idx < (uint32_t)LV_CAP) L.stage[rq.kw * LV_S + idx] = (uint16_t)(v - lo);
-                    else atomicOr(&m.flags, LV_REDO | LV_WHY(6));
-                }
-            }
         }
         wave_sync();
     }
@@ -1981,7 +1717,6 @@ struct svt_ctx {
     svt_params prm{};
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
-    bool ix_exact = false;        // SVTREK_IX_EXACT=1: every index range takes the exact census (tests)
     uint64_t ix_ranges = 65536;   // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
     int lane_w = 0;               // SVTREK_LANE_W=8|32 forces the lane kernel's windows per wave (A/B)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
@@ -1998,13 +1733,11 @@ struct svt_ctx {
     int64_t *d_tid_off = nullptr, *d_bkt_off = nullptr;
     uint2 *d_bkt = nullptr;
     uint32_t *d_cigar = nullptr;      // CIGAR stream
-    uint64_t *d_insbase = nullptr;    // per read: its first I >= 50 op's index in the insertion sequences
-    uint64_t n_ins = 0;               // I >= 50 ops in the pileup
+    uint64_t n_ins = 0;               // I >= 50 ops in the pileup (= I-list events; d_spoffI indexes them per read)
     // device index (svt_index.inc)
     uint64_t *d_part = nullptr;       // [n_ranges + 1]
     uint32_t n_ranges = 0;
     IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan
-    uint32_t *d_xlist = nullptr;      // [n_ranges] ranges for the exact census
     uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
     uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
     int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
@@ -2012,16 +1745,14 @@ struct svt_ctx {
     uint64_t *d_tot = nullptr;
     void *d_scan_tmp = nullptr;       // hipcub scan scratch
     size_t scan_tmp_bytes = 0;
-    uint32_t *d_lchunk = nullptr;
-    uint64_t n_evD = 0, n_evI = 0, n_slow = 0, n_lead_blocks = 0;
-    uint64_t lchunk_units = 0;        // lead chunk area: ix_unit(n_stream, n_reads) + 2 16-B units
+    uint64_t n_evD = 0, n_evI = 0;
     // allele-consensus mode (svt_load_insseq / svt_poa_consensus)
     uint64_t *d_ins_off = nullptr;
     uint8_t *d_ins_bases = nullptr;
     bool insseq_loaded = false;
     PoaPool poa_small, poa_big;       // POA scratch slots (poa_pool)
     uint64_t poa_deferred = 0;        // loci the last svt_poa_consensus reran on full-size slots
-    uint64_t *d_spoffD = nullptr, *d_spoffI = nullptr, *d_slowpre = nullptr;   // span walk
+    uint64_t *d_spoffD = nullptr, *d_spoffI = nullptr;   // span walk
     uint4 *d_spD = nullptr, *d_spI = nullptr;
     uint64_t dev_bytes = 0;
     bool loaded = false;
@@ -2123,23 +1854,25 @@ svt_status grow_pool(svt_ctx *c) {
 void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
-    hfree(c->d_insbase); hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_xlist); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
-    hfree(c->d_lchunk);
+    hfree(c->d_ins_off); hfree(c->d_ins_bases);
+    hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
     c->scan_tmp_bytes = 0;
-    hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_slowpre); hfree(c->d_spD); hfree(c->d_spI);
+    hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
-    c->n_evD = c->n_evI = c->n_slow = c->n_lead_blocks = c->lchunk_units = 0;
+    c->n_evD = c->n_evI = 0;
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
 }
 
 KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t n, bool count) {
     KArgs a;
     a.pile = DevPileup{c->d_pos, c->d_emax, c->d_rec, c->d_off64, c->d_tid_off, c->d_bkt_off, c->d_bkt,
-                       c->d_cigar, c->d_lchunk, c->d_insbase, c->d_spoffD, c->d_spoffI,
-                       c->d_spD, c->d_spI, c->d_slowpre, c->n_targets};
-    a.prm = KParams{c->prm.wider_interval, c->prm.median_interval, c->prm.narrow_interval,
-                    c->prm.consensus_interval_range, c->prm.consensus_interval, c->prm.consensus_min_count, 0, 0};
+                       c->d_cigar, c->d_spoffD, c->d_spoffI, c->d_spD, c->d_spI, c->n_targets};
+    const svt_params &q = c->prm;
+    // KParams::sent_ok: narrow + 2 >= max(range + max(ci, 0), 26) (64-bit: any int32 parameters)
+    const int64_t width = std::max<int64_t>((int64_t)q.consensus_interval_range + std::max<int64_t>(q.consensus_interval, 0),
+                                            SV_MIN_LENGTH / 2 + 1);
+    a.prm = KParams{q.wider_interval, q.median_interval, q.narrow_interval, q.consensus_interval_range,
+                    q.consensus_interval, q.consensus_min_count, 0, 0, (int64_t)q.narrow_interval + 2 >= width ? 1 : 0};
     a.loci = d_loci;
     a.out = d_out;
     a.n = n;
@@ -2334,7 +2067,7 @@ svt_status poa_run(svt_ctx *c, const svt_poa_params *p, const svt_locus *loci, c
         a.loci = d_loci;
         a.refined = d_ref;
         a.n = (uint32_t)n;
-        a.ins_base = c->d_insbase;
+        a.ins_base = c->d_spoffI;
         a.ins_off = c->d_ins_off;
         a.ins_bases = c->d_ins_bases;
         a.cap = cap;
@@ -2392,7 +2125,6 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     c->prm = *params;
     const char *g = getenv("SVTREK_GATHER");   // "span1": the one-wave-per-window kernel at every batch size
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
-    if (const char *x = getenv("SVTREK_IX_EXACT")) c->ix_exact = atoi(x) == 1;
     if (const char *x = getenv("SVTREK_IX")) c->ix_mode = strcmp(x, "lane") == 0 ? 1 : strcmp(x, "stream") == 0 ? 2 : 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
@@ -2420,7 +2152,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     // load the code object now (HIP loads it lazily at the first launch), so that no later
     // call -- and no timing of one -- pays for it
     hipFuncAttributes fa;
-    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(index_kernel<false>));
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(index_kernel));
     *out = c;
     return SVT_OK;
 }
@@ -2466,8 +2198,8 @@ void parallel_for(size_t n, size_t cap, F fn) {
     for (auto &x : th) x.join();
 }
 
-// The device index of the loaded pileup (svt_index.inc): census (with the ranges' look-back
-// scan), then emit.  `first`: size and allocate the event lists and the lead chunks from the
+// The device index of the loaded pileup (svt_index.inc / svt_index2.inc): census, exclusive
+// scan of the range (group) totals, emit.  `first`: size and allocate the event lists from the
 // totals (one synchronous read-back); later calls (svt_reindex) reuse them -- the totals depend
 // on the pileup only.  `ms`: the index kernels' device time (HIP events; the read-back and
 // allocations excluded).
@@ -2481,20 +2213,12 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.wbase = c->d_wbase;
     a.spoffD = c->d_spoffD;
     a.spoffI = c->d_spoffI;
-    a.insbase = c->d_insbase;
-    a.slowpre = c->d_slowpre;
     a.spD = c->d_spD;
     a.spI = c->d_spI;
-    a.lchunk = c->d_lchunk;
     a.capD = c->n_evD;
     a.capI = c->n_evI;
-    a.capL = c->lchunk_units * 4u;
     a.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
-    a.xlist = c->d_xlist;
-    a.xcnt = (uint32_t *)(c->d_ctl + CTL_XCNT);
-    a.exact_all = c->ix_exact ? 1u : 0u;
     a.n_ranges = c->n_ranges;
-    const dim3 grid((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block(64 * IX_WPB);
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (ms)
         for (auto &e : ev) HIP_TRY(c, hipEventCreate(&e));
@@ -2505,30 +2229,25 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     };
     // lane per read (svt_index2.inc) for short reads -- a wave's 64 reads then take a few steps
     // each; long reads (a lane walking thousands of ops waits on its loads) take the stream walk,
-    // which spreads every slot of 256 ops over the wave (cfg4 28 ops/read: lane 1.15 vs stream
-    // 1.24 ms; cfg5 1715 ops/read: lane 31.1 vs stream 18.7 ms); never for a group of > 2^27 ops
+    // which spreads every slot of 256 ops over the wave; never for a group of > 2^27 ops
     const bool lane = c->n_groups > 0 && (c->ix_mode == 1 || (c->ix_mode == 0 && c->n_ops <= 64ull * c->n_reads));
     c->load_stats.index_kind = lane ? 1u : 2u;
     const uint32_t nparts = lane ? c->n_groups : c->n_ranges;   // what the scan runs over
     Ix2Args a2{a, c->d_cnt, (uint64_t)c->n_reads, c->n_groups};
     const dim3 grid2((unsigned)((c->n_groups + IX2_WPB - 1) / IX2_WPB)), block2(64 * IX2_WPB);
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
-    if (lane) {
+    if (lane)
         hipLaunchKernelGGL(ix2_census_kernel, grid2, block2, 0, st, a2);
-    } else {
+    else
         hipLaunchKernelGGL(ix_census_kernel, dim3((unsigned)((c->n_ranges + IXC_WPB - 1) / IXC_WPB)), dim3(64 * IXC_WPB), 0,
                            st, a);
-        hipLaunchKernelGGL(index_kernel<false>, dim3((unsigned)std::min<uint32_t>(IX_XGRID, (c->n_ranges + IX_WPB - 1) / IX_WPB)),
-                           block, 0, st, a);
-    }
     hipError_t e = hipGetLastError();
     if (e == hipSuccess)   // the ranges' / groups' exclusive prefixes
         e = hipcub::DeviceScan::ExclusiveScan(c->d_scan_tmp, c->scan_tmp_bytes, c->d_agg, c->d_wbase, IxTotSum(),
                                               IxTot{}, (int)nparts, st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(ix_totals_kernel, dim3(1), dim3(64), 0, st, (const IxTot *)c->d_agg,
-                           (const IxTot *)c->d_wbase, nparts, c->d_tot, c->d_spoffD, c->d_spoffI, c->d_insbase,
-                           c->d_slowpre, (uint64_t)c->n_reads, a.xcnt);
+                           (const IxTot *)c->d_wbase, nparts, c->d_tot, c->d_spoffD, c->d_spoffI, (uint64_t)c->n_reads);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index census: %s", hipGetErrorString(e)));
@@ -2540,24 +2259,19 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
         if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index totals: %s", hipGetErrorString(e)));
         c->n_evD = t[IX_D];
         c->n_evI = t[IX_I];
-        c->n_ins = t[IX_INS];
-        c->n_slow = t[IX_SLOW];
-        c->n_lead_blocks = t[IX_LB];
+        c->n_ins = t[IX_I];
         svt_status s;
         if ((s = upload<uint4>(c, c->d_spD, nullptr, 0, std::max<uint64_t>(c->n_evD, 1)))) return done(s);
         if ((s = upload<uint4>(c, c->d_spI, nullptr, 0, std::max<uint64_t>(c->n_evI, 1)))) return done(s);
-        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, c->lchunk_units * 4u + LEAD_PAD))) return done(s);
         a.spD = c->d_spD;
         a.spI = c->d_spI;
-        a.lchunk = c->d_lchunk;
         a.capD = c->n_evD;
         a.capI = c->n_evI;
-        a.capL = c->lchunk_units * 4u;
         a2.a = a;
     }
     if (ms && hipEventRecord(ev[2], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     if (lane) hipLaunchKernelGGL(ix2_emit_kernel, grid2, block2, 0, st, a2);
-    else hipLaunchKernelGGL(index_kernel<true>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(index_kernel, dim3((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), dim3(64 * IX_WPB), 0, st, a);
     e = hipGetLastError();
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index emit: %s", hipGetErrorString(e)));
     if (ms) {
@@ -2620,7 +2334,6 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
             if (p->endpos[r] > m) m = p->endpos[r];
             maxpos = std::max(maxpos, p->pos[r]);
             emax[(size_t)r] = m;
-            // SLOW_BIT is set by the index census on the device
             rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | (clip << 30), 0u);
         }
         zeros[t] = z;
@@ -2666,9 +2379,6 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         strm = strm2.data();
     }
     const uint64_t nstream = nr > 0 ? soff[nr] : 0;
-    c->lchunk_units = ix_unit(nstream, (uint64_t)nr) + 2u;
-    if (c->lchunk_units >= (1ull << 32))   // a lead event's unit index is 32 bits
-        return fail(c, SVT_EINVAL, "pileup: %s", ">= 2^32 lead chunk units (2^36 stream ops)");
     // ---- ranges of the index build: ~T stream ops each, cut at read starts and contig starts
     const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / c->ix_ranges, 2048), 1ull << 26);
     std::vector<std::vector<uint64_t>> pt((size_t)nt);
@@ -2703,12 +2413,9 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
     if ((s = upload(c, c->d_cigar, strm, (size_t)nstream, STREAM_PAD))) return s;
     if ((s = upload(c, c->d_part, part.data(), part.size()))) return s;
-    if ((s = upload<uint32_t>(c, c->d_xlist, nullptr, 0, std::max<size_t>(part.size() - 1, 1)))) return s;
     const size_t S = (size_t)nr + 1;
     if ((s = upload<uint64_t>(c, c->d_spoffD, nullptr, 0, S))) return s;
     if ((s = upload<uint64_t>(c, c->d_spoffI, nullptr, 0, S))) return s;
-    if ((s = upload<uint64_t>(c, c->d_insbase, nullptr, 0, S))) return s;
-    if ((s = upload<uint64_t>(c, c->d_slowpre, nullptr, 0, S))) return s;
     if ((s = upload<uint2>(c, c->d_cnt, nullptr, 0, std::max<size_t>((size_t)nr, 1)))) return s;
     const size_t NR = std::max<size_t>({(size_t)c->n_ranges, (size_t)c->n_groups, (size_t)1});
     if ((s = upload<IxTot>(c, c->d_agg, nullptr, 0, NR))) return s;
@@ -2733,19 +2440,17 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         c->load_stats.index_ms = ims;
         const uint64_t R = (uint64_t)nr;
         c->load_stats.span_events = c->n_evD + c->n_evI;
-        c->load_stats.lead_blocks = c->n_lead_blocks;
-        c->load_stats.slow_reads = c->n_slow;
+        c->load_stats.lead_blocks = 0;   // (no lead chunks since 0.17: refine_end's stops vote as e + 2)
+        c->load_stats.slow_reads = 0;    // (no slow reads since 0.17: walks saturate at 2^30)
         // lane per read: census stream + soff + rec (24 B/read), cnt written (8 B/read); emit cnt
-        // + soff + rec (32 B/read) + stream, the per-read offsets (32 B/read) written.  Stream
+        // + soff + rec (32 B/read) + stream, the per-read offsets (16 B/read) written.  Stream
         // walk: census stream + rec (16 B/read); emit stream + soff + rec (24 B/read), offsets.
-        // Both: the events and lead units written.
-        const uint64_t per_read = c->load_stats.index_kind == 1 ? 96u : 72u;
-        c->load_stats.index_bytes = 8ull * nstream + per_read * R +
-                                    16ull * (c->n_evD + c->n_evI) + 16ull * c->n_lead_blocks;
+        // Both: the events written.
+        const uint64_t per_read = c->load_stats.index_kind == 1 ? 80u : 56u;
+        c->load_stats.index_bytes = 8ull * nstream + per_read * R + 16ull * (c->n_evD + c->n_evI);
     } else {
         for (auto *pp : {&c->d_spD, &c->d_spI})
             if ((s = upload<uint4>(c, *pp, nullptr, 0, 1))) return s;
-        if ((s = upload<uint32_t>(c, c->d_lchunk, nullptr, 0, LEAD_PAD))) return s;
     }
     HIP_TRY(c, hipDeviceSynchronize());
     {
@@ -3072,6 +2777,9 @@ svt_status svt_bgzf_inflate_device(svt_ctx *c, const uint8_t *d_comp, const svt_
     const unsigned grid = (unsigned)std::min<size_t>((n + WAVE - 1) / WAVE, (size_t)INF_GRID);
     if (!c->d_infs) HIP_TRY(c, hipMalloc(&c->d_infs, (size_t)INF_GRID * WAVE * sizeof(InfSlow)));
     if (!c->d_inferr) HIP_TRY(c, hipMalloc(&c->d_inferr, sizeof(uint32_t)));
+    // the scratch slots and the error word are per context: calls on different streams run in
+    // submission order (like every other launch of the context)
+    if (svt_status s = order_on(c, st)) return s;
     HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), st));
     hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, st, d_comp, d_blocks, (uint32_t)n, d_out, c->d_infs,
                        c->d_inferr);
@@ -3084,8 +2792,11 @@ svt_status svt_bgzf_inflate_status(svt_ctx *c, void *stream, uint32_t *bad_block
     *bad_block = 0xffffffffu;
     if (!c->d_inferr) return SVT_OK;
     DEV_GUARD(c);
-    HIP_TRY(c, hipMemcpyAsync(bad_block, c->d_inferr, sizeof(uint32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
-    HIP_TRY(c, hipStreamSynchronize((hipStream_t)stream));
+    // the error word belongs to the context's last inflate: order after it, whatever its stream
+    const hipStream_t st = (hipStream_t)stream;
+    if (svt_status s = order_on(c, st)) return s;
+    HIP_TRY(c, hipMemcpyAsync(bad_block, c->d_inferr, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
     if (*bad_block != 0xffffffffu) {
         char m[64];
         snprintf(m, sizeof m, "%u", *bad_block);

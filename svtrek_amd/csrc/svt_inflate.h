@@ -118,19 +118,25 @@ SVT_HD uint32_t inf_rev(uint32_t code, int len) {   // reverse the low len bits
 }
 
 // Build a table from n code lengths: primary entries (tab, 1 << bits) + slow-path arrays.
-// False for an over-subscribed code (an incomplete code is allowed, as zlib allows it for the
-// distance code with one symbol).
+// False for a code zlib's inflate_table rejects (inftrees.c): over-subscribed, or incomplete
+// where it is not allowed -- kind INF_CODES (the code-length code) never, INF_LENS (litlen and
+// distance codes) only for a single code of length 1; a code with no symbols at all is built
+// (every lookup fails, as zlib's "invalid code" table does).  INF_FIXED: the fixed codes (their
+// 30 distance codes of 5 bits are short of the 32 zlib builds; the 2 unused ones never occur).
+constexpr int INF_FIXED = 0, INF_CODES = 1, INF_LENS = 2;
 SVT_HD bool inf_build(const uint8_t *len, int n, const InfTab tab, int bits, uint16_t *cnt, uint16_t *sym,
-                      uint16_t *offs) {
+                      uint16_t *offs, int kind) {
     for (int i = 0; i < 16; i++) cnt[i] = 0;
     for (int s = 0; s < n; s++) cnt[len[s]]++;
     cnt[0] = 0;
-    int left = 1;
+    int left = 1, max = 0;
     for (int l = 1; l < 16; l++) {
         left <<= 1;
         left -= cnt[l];
-        if (left < 0) return false;
+        if (left < 0) return false;   // over-subscribed
+        if (cnt[l]) max = l;
     }
+    if (kind != INF_FIXED && max > 0 && left > 0 && (kind == INF_CODES || max != 1)) return false;   // incomplete
     offs[1] = 0;
     for (int l = 1; l < 15; l++) offs[l + 1] = (uint16_t)(offs[l] + cnt[l]);
     for (int s = 0; s < n; s++)
@@ -216,8 +222,8 @@ SVT_HD int inf_block(const InfV4 *in, uint32_t skip, uint32_t clen, uint8_t *out
             if (type == 1) {   // fixed codes (RFC 1951 3.2.6)
                 for (int s = 0; s < 288; s++) S.len[s] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
                 for (int s = 0; s < 30; s++) S.len[288 + s] = 5;
-                inf_build(S.len, 288, F.lit, IF_LB, S.lcnt, S.lsym, S.offs);
-                inf_build(S.len + 288, 30, F.dst, IF_DB, S.dcnt, S.dsym, S.offs);
+                inf_build(S.len, 288, F.lit, IF_LB, S.lcnt, S.lsym, S.offs, INF_FIXED);
+                inf_build(S.len + 288, 30, F.dst, IF_DB, S.dcnt, S.dsym, S.offs, INF_FIXED);
             } else {           // dynamic codes (3.2.7)
                 br.fill();
                 const int nlen = (int)br.get(5) + 257, ndist = (int)br.get(5) + 1, ncode = (int)br.get(4) + 4;
@@ -228,7 +234,7 @@ SVT_HD int inf_block(const InfV4 *in, uint32_t skip, uint32_t clen, uint8_t *out
                     S.cl[inf_ord(i)] = (uint8_t)br.get(3);
                 }
                 // the code-length code: 7-bit table in the litlen table's place
-                if (!inf_build(S.cl, 19, F.lit, 7, S.lcnt, S.lsym, S.offs)) return INF_EDATA;
+                if (!inf_build(S.cl, 19, F.lit, 7, S.lcnt, S.lsym, S.offs, INF_CODES)) return INF_EDATA;
                 int i = 0;
                 while (i < nlen + ndist) {
                     br.fill();
@@ -256,8 +262,8 @@ SVT_HD int inf_block(const InfV4 *in, uint32_t skip, uint32_t clen, uint8_t *out
                 // (the dist lengths move to 288.. so that both live in S.len while building)
                 for (int k = ndist - 1; k >= 0; k--) S.len[288 + k] = S.len[nlen + k];
                 for (int k = nlen; k < 288; k++) S.len[k] = 0;
-                if (!inf_build(S.len, 288, F.lit, IF_LB, S.lcnt, S.lsym, S.offs)) return INF_EDATA;
-                if (!inf_build(S.len + 288, ndist, F.dst, IF_DB, S.dcnt, S.dsym, S.offs)) return INF_EDATA;
+                if (!inf_build(S.len, 288, F.lit, IF_LB, S.lcnt, S.lsym, S.offs, INF_LENS)) return INF_EDATA;
+                if (!inf_build(S.len + 288, ndist, F.dst, IF_DB, S.dcnt, S.dsym, S.offs, INF_LENS)) return INF_EDATA;
             }
             // literals are combined into 4-byte stores at 4-byte aligned output addresses (wc holds
             // the wn bytes of the current word, from out[op - wn]); a match or the block's end

@@ -86,3 +86,23 @@ def test_inflate_cpu_backend_agrees(tmp_path):
     b = cpu.bgzf_inflate(comp, blocks)
     cpu.close()
     assert a.tobytes() == b.tobytes() == _zlib_all(comp, blocks)
+
+
+def test_inflate_incomplete_codes_as_zlib(engine_factory):
+    """Hand-built dynamic blocks on the device: an incomplete code-length code and
+    an incomplete literal/length code are rejected as zlib rejects them (the host path and the
+    reference's htslib inflate with zlib), a lone 1-bit distance code is accepted."""
+    from test_inflate_core import _dynamic_block, _zlib_ok
+    data = b"SVTrek"
+    eng = engine_factory()
+    for cl, lit, valid in (({9: 1, 1: 2, 2: 2}, [9] * 256 + [1], True), ({9: 1, 1: 2}, [9] * 256 + [1], False),
+                           ({9: 1, 2: 2, 1: 2}, [9] * 256 + [2], False)):
+        comp = _dynamic_block(cl, lit, [1], data)
+        assert _zlib_ok(comp, len(data)) == valid
+        blocks = np.array([(3, 0, len(comp), len(data))], dtype=BGZF_BLOCK_DTYPE)
+        buf = bytes(3) + comp
+        if valid:
+            assert eng.bgzf_inflate(buf, blocks).tobytes() == data
+        else:
+            with pytest.raises(RuntimeError, match="corrupt BGZF block 0"):
+                eng.bgzf_inflate(buf, blocks)

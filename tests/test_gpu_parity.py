@@ -462,42 +462,58 @@ def test_size_based_kernel_pick_alternating(engine_factory):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_index_census_streaming_vs_exact(engine_factory, seed):
-    """The index builds agree: lane per read (the product's pick for short reads; also forced;
-    its census streams each 64-read group and falls back to the per-lane walk where a slow read
-    is possible -- SVTREK_IX_EXACT=1 forces that walk everywhere), the stream walk
-    (SVTREK_IX=stream: ranges whose op lengths cannot reach a slow walk take the streaming
-    census, the others the exact per-slot census) and the stream walk with every range forced
-    through the exact census (SVTREK_IX_EXACT=1).  A pileup with slow reads in a few places (so
-    both kinds of range occur): same index sizes, same results as the oracle, also after a
-    rebuild from the resident pileup."""
+def test_index_kinds_agree_with_saturating_walks(engine_factory, seed):
+    """The two index builds agree: lane per read (the product's pick for short reads; also
+    forced, SVTREK_IX=lane) and the stream walk (SVTREK_IX=stream), with and without the stream
+    walk's quiet slots (long reads, SVTREK_IX_RANGES=1: a few huge ranges).  The pileup has reads
+    whose walks pass 2^28 and 2^30 (huge H ops, refinement.c:141 advances on H): the index
+    saturates their walk positions at 2^30, windows ending below 2^30 stay exact on them, and
+    windows ending past 2^30 take the per-read replay.  Same index sizes, same results as the
+    oracle, also after a rebuild from the resident pileup."""
     from svtrek_amd.pileup import from_reads
     rng = np.random.default_rng(50 + seed)
     rows = []
     big = (1 << 28) - 1
     pos = 5000
+    far = []   # (walk position, endpos) regions reached through huge N ops
     for i in range(4000):
         pos += int(rng.integers(0, 40))
-        n = int(rng.integers(1, 30))
-        ops = [(int(rng.choice([0, 1, 2, 4, 5])), int(rng.integers(1, 120))) for _ in range(n)]
-        if i % 997 == 3:                       # a slow read: its walk passes 2^28
-            ops += [(5, big), (2, 60), (0, 5)]
+        if i % 50:
+            ops = [(int(rng.choice([0, 1, 2, 4, 5, 0, 0, 8])), int(rng.integers(1, 120)))
+                   for _ in range(int(rng.integers(1, 30)))]
+        else:   # a long read with few candidates: quiet slots of the stream walk
+            ops = [(int(rng.choice([0, 0, 0, 8, 1, 2, 7])), int(rng.integers(1, 20)))
+                   for _ in range(int(rng.integers(300, 3000)))]
+            for _ in range(int(rng.integers(0, 3))):
+                ops.insert(int(rng.integers(0, len(ops))), (int(rng.choice([1, 2])), int(rng.integers(50, 400))))
+        if i % 997 == 3:     # a walk past 2^28 / 2^30 on huge H ops (the walk runs ahead of endpos)
+            ops += [(5, big)] * (1 if i % 2 else 5) + [(2, 60), (0, 5)]
+        if i % 991 == 5:     # ... and on huge N ops (endpos follows: windows out there see the read)
+            k = 3 if i % 2 else 4
+            ops = [(0, 100)] + [(3, big)] * k + [(2, 60), (0, 50), (4, 30)]
+            far.append(pos + 100 + k * big)
         if rng.random() < 0.3:
             ops = [(4, int(rng.integers(1, 40)))] + ops
+        if rng.random() < 0.3:
+            ops = ops + [(4, int(rng.integers(1, 40)))]
         rows.append((0, pos, ops))
     pl = from_reads(1, rows)
     hot = [int(x) for x in rng.integers(6000, pos, size=8)]
     loci = random_loci(rng, 400, 1, pos + 2000, hot)
+    extra = [(2, 1, (1 << 30) - 3000, (1 << 30) + 100), (1, 1, (1 << 30) - 50, 0)]
+    for f in far:   # DEL / INS calls at the far D ops: below and past 2^30
+        extra += [(2, 1, f + int(d), f + 60 + int(d)) for d in rng.integers(-5, 5, 3)] + [(1, 1, f, 0)]
+    loci = np.concatenate([loci, make_loci(extra)])
     want = O.refine_batch(pl, loci)
     stats = []
-    for env in (None, {"SVTREK_IX": "lane"}, {"SVTREK_IX": "lane", "SVTREK_IX_EXACT": "1"},
-                {"SVTREK_IX": "stream"}, {"SVTREK_IX": "stream", "SVTREK_IX_EXACT": "1"}):
+    for env in (None, {"SVTREK_IX": "lane"}, {"SVTREK_IX": "stream"},
+                {"SVTREK_IX": "stream", "SVTREK_IX_RANGES": "1"}):
         eng = engine_factory(env=env)
         eng.load_pileup(pl)
         st = eng.load_stats()
-        stats.append((st["span_events"], st["lead_blocks"], st["slow_reads"]))
+        stats.append(st["span_events"])
         _assert_same(eng.refine(loci), want, loci)
         for _ in range(2):   # rebuilds from the resident pileup
             eng.reindex()
             _assert_same(eng.refine(loci), want, loci)
-    assert all(x == stats[0] for x in stats) and stats[0][2] >= 4
+    assert all(x == stats[0] for x in stats)

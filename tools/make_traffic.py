@@ -34,14 +34,26 @@ def med(v: list[float]) -> float | None:
 
 
 STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's kernel name); the
-           # index build is either the lane-per-read pair (default) or the stream walk (SVTREK_IX=stream)
+           # index build is either the lane-per-read pair (short reads) or the stream walk (long reads)
     "ix2_census_kernel": "ix2_census_kernel",
     "ix2_emit_kernel": "ix2_emit_kernel",
     "ix_census_kernel": "(anonymous namespace)::ix_census_kernel",
-    "index_kernel<emit>": "index_kernel<true>",
+    "index_kernel": "(anonymous namespace)::index_kernel(",
     "refine_lane_kernel": "refine_lane_kernel",
     "refine_redo_kernel": "refine_redo_kernel",
 }
+
+
+def kernel_avg_ns(src: str, kernel: str) -> float | None:
+    """Average duration of the kernel in the run's rocprofv3 --stats summary (trace/)."""
+    path = os.path.join(src, "trace", "run_kernel_stats.csv")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r["Name"]:
+                return float(r["AverageNs"])
+    return None
 
 
 def kernel_bytes(src: str, kernel: str) -> dict | None:
@@ -100,8 +112,9 @@ def main() -> int:
         kb = kernel_bytes(a.src, sub)
         if kb is None:
             continue
+        ns = kernel_avg_ns(a.src, sub)
         e = {"kernel": label, "records": True, "workload": a.workload, "engine_version": ver, **kb,
-             "source": f"{a.dst}/pmc_*.csv"}
+             "avg_ns": ns, "source": f"{a.dst}/pmc_*.csv, {a.dst}/kernel_stats.csv"}
         new.append(e)
         for k in step:
             step[k] += kb[k]
