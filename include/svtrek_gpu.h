@@ -317,6 +317,40 @@ double svt_bgzf_last_inflate_ms(const svt_ctx *ctx);
 void *svt_host_alloc(svt_ctx *ctx, size_t bytes);
 void  svt_host_free(svt_ctx *ctx, void *p);
 
+/* ---- BAM records decoded on the device ---------------------------------
+ * Replaces, for this path, htslib's bam_read1 behind every sam_itr_next (reference
+ * refinement.c:117; the path reads core.tid/pos/flag/n_cigar and the CIGAR, :118-120) and the
+ * host ingest's record parse: the BAM's BGZF blocks go to the device compressed, are inflated
+ * there, and their records are found, parsed (CG:B,I CIGARs restored as htslib's bam_tag2cigar
+ * does) and appended to a device-resident columnar pileup -- no inflated byte crosses PCIe.
+ * Records with tid < 0 / tid >= n_targets / pos < 0 are skipped (no tid >= 0 query yields them).
+ *   svt_bam_dec_open:  a decoder on ctx's device for a BAM with n_targets references;
+ *   svt_bam_dec_feed:  the next batch of whole BGZF blocks of the file, in order (host buffers,
+ *                      the layout of svt_bgzf_inflate, uoff relative to the batch); the first
+ *                      `skip` inflated bytes of the first batch are the BAM header (not records);
+ *                      a record may span batches.  Synchronous.
+ *   svt_bam_dec_load:  at the end of the file: the decoded pileup becomes ctx's pileup, exactly
+ *                      as svt_load_pileup of the same reads (a file not sorted by coordinate is
+ *                      sorted, as the host ingest does); SVT_EINVAL for a truncated last record.
+ * Errors: SVT_EINVAL for a corrupt BGZF block or BAM record (message in svt_last_error(ctx)). */
+typedef struct svt_bam_dec svt_bam_dec;
+typedef struct svt_bam_dec_stats {
+    uint64_t records;         /* complete records decoded (all tids)                          */
+    uint64_t reads;           /* records kept for the pileup                                  */
+    uint64_t cigar_ops;       /* their CIGAR ops (after CG restoration)                        */
+    uint64_t cg_restored;     /* CIGARs restored from a CG:B,I tag                             */
+    uint64_t batches;         /* svt_bam_dec_feed calls                                       */
+    uint64_t rechained;       /* batches whose record starts were re-chained hop by hop        */
+    uint64_t inflated_bytes;  /* bytes the batches inflated to                                 */
+    double   feed_ms;         /* wall time inside svt_bam_dec_feed (H2D, inflate, decode)       */
+} svt_bam_dec_stats;
+svt_status svt_bam_dec_open(svt_ctx *ctx, int32_t n_targets, svt_bam_dec **out);
+svt_status svt_bam_dec_feed(svt_bam_dec *dec, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
+                            size_t n, uint64_t skip);
+svt_status svt_bam_dec_load(svt_bam_dec *dec);
+svt_status svt_bam_dec_stats_get(const svt_bam_dec *dec, svt_bam_dec_stats *out);
+void       svt_bam_dec_close(svt_bam_dec *dec);
+
 const char *svt_last_error(const svt_ctx *ctx);
 void        svt_close(svt_ctx *ctx);
 const char *svt_version(void);

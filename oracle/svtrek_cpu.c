@@ -267,3 +267,226 @@ void svt_close(svt_ctx *c) {
     free(c);
 }
 const char *svt_version(void) { return "svtrek_cpu (oracle restatement, test infrastructure)"; }
+
+/* ---- svt_bam_dec_*: the BAM decoded record by record on the host (a plain-C restatement of
+ * htslib's bam_read1 + bam_tag2cigar for the fields the path reads, refinement.c:117-120), so
+ * that the CLI's decode flow runs on this backend too and cross-checks the device decoder. */
+struct svt_bam_dec {
+    svt_ctx *c;
+    int32_t n_ref;
+    int first;
+    uint8_t *buf;              /* inflated bytes not consumed yet (an incomplete record) */
+    size_t n, cap;
+    int32_t *tid, *pos, *endpos;
+    uint8_t *clip;
+    uint64_t *cig_off;
+    uint32_t *cigar;
+    size_t nr, rcap, nw, wcap;
+    svt_bam_dec_stats st;
+};
+
+static uint32_t bd_rd32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+static uint32_t bd_rd16(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
+
+/* the CG:B,I array of a record's aux fields (htslib bam_tag2cigar's lookup) */
+static int bd_find_cg(const uint8_t *p, const uint8_t *end, const uint8_t **arr, uint32_t *cnt) {
+    while (p + 3 <= end) {
+        const char t0 = (char)p[0], t1 = (char)p[1], ty = (char)p[2];
+        p += 3;
+        if (ty == 'A' || ty == 'c' || ty == 'C') { p += 1; continue; }
+        if (ty == 's' || ty == 'S') { p += 2; continue; }
+        if (ty == 'i' || ty == 'I' || ty == 'f') { p += 4; continue; }
+        if (ty == 'Z' || ty == 'H') {
+            while (p < end && *p) p++;
+            if (p >= end) return 0;
+            p++;
+            continue;
+        }
+        if (ty != 'B' || p + 5 > end) return 0;
+        const char sub = (char)p[0];
+        const uint32_t n = bd_rd32(p + 1);
+        const size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2
+                          : (sub == 'i' || sub == 'I' || sub == 'f') ? 4 : 0;
+        if (!es) return 0;
+        if (t0 == 'C' && t1 == 'G') {
+            if ((sub != 'I' && sub != 'i') || p + 5 + (size_t)n * 4 > end) return 0;
+            *arr = p + 5;
+            *cnt = n;
+            return 1;
+        }
+        p += 5 + (size_t)n * es;
+    }
+    return 0;
+}
+
+static int bd_grow(void **p, size_t *cap, size_t need, size_t elem) {
+    if (need <= *cap) return 1;
+    size_t nc = *cap ? *cap : 1024;
+    while (nc < need) nc += nc / 2 + 1;
+    void *q = realloc(*p, nc * elem);
+    if (!q) return 0;
+    *p = q;
+    *cap = nc;
+    return 1;
+}
+
+/* One complete record (r: after its block_size word) -> the columns; 0 = corrupt. */
+static int bd_take(svt_bam_dec *d, const uint8_t *r, uint32_t bs) {
+    const uint8_t *rend = r + bs;
+    const int32_t tid = (int32_t)bd_rd32(r), pos = (int32_t)bd_rd32(r + 4);
+    const uint32_t l_qname = r[8], n_cig = bd_rd16(r + 12), flag = bd_rd16(r + 14);
+    const int32_t l_seq = (int32_t)bd_rd32(r + 16);
+    d->st.records++;
+    if (!(tid >= 0 && tid < d->n_ref && pos >= 0)) return 1;   /* no tid >= 0 query yields it */
+    const uint8_t *qn = r + 32, *cg = qn + l_qname;
+    if (cg + 4ull * n_cig > rend || l_seq < 0) return 0;
+    const uint8_t *after = cg + 4ull * n_cig, *aux = after + (size_t)(l_seq + 1) / 2 + (size_t)l_seq;
+    const uint8_t *cig = cg;
+    uint32_t n = n_cig;
+    if (n_cig > 0 && (bd_rd32(cg) & 0xfu) == 4u && (int64_t)(bd_rd32(cg) >> 4) == l_seq && aux <= rend) {
+        const uint8_t *arr;
+        uint32_t cnt;
+        if (bd_find_cg(aux, rend, &arr, &cnt) && cnt >= n_cig && cnt < (1u << 29)) { cig = arr; n = cnt; d->st.cg_restored++; }
+    }
+    uint8_t clip = 0;   /* the words refinement.c:120 and :210 test (the padded name / first SEQ byte for n == 0) */
+    if (n) {
+        if ((bd_rd32(cig + 4ull * (n - 1)) & 0xfu) == 4u) clip |= SVT_CLIP_LAST_S;
+        if ((bd_rd32(cig) & 0xfu) == 4u) clip |= SVT_CLIP_FIRST_S;
+    } else {
+        const uint32_t padded = (l_qname + 3u) & ~3u;
+        const uint8_t w0 = (padded >= 4 && padded - 4 < l_qname) ? qn[padded - 4] : 0;
+        if ((w0 & 0xfu) == 4u) clip |= SVT_CLIP_LAST_S;
+        if (after < rend && (after[0] & 0xfu) == 4u) clip |= SVT_CLIP_FIRST_S;
+    }
+    if (d->nr + 1 > d->rcap) {   /* every per-read column to the same capacity */
+        const size_t nc = d->rcap ? d->rcap + d->rcap / 2 : 1024;
+        int32_t *t = (int32_t *)realloc(d->tid, nc * sizeof(int32_t));
+        if (t) d->tid = t;
+        int32_t *ps = (int32_t *)realloc(d->pos, nc * sizeof(int32_t));
+        if (ps) d->pos = ps;
+        int32_t *ep = (int32_t *)realloc(d->endpos, nc * sizeof(int32_t));
+        if (ep) d->endpos = ep;
+        uint8_t *cl = (uint8_t *)realloc(d->clip, nc);
+        if (cl) d->clip = cl;
+        uint64_t *co = (uint64_t *)realloc(d->cig_off, nc * sizeof(uint64_t));
+        if (co) d->cig_off = co;
+        if (!t || !ps || !ep || !cl || !co) return 0;
+        d->rcap = nc;
+    }
+    if (!bd_grow((void **)&d->cigar, &d->wcap, d->nw + n + 1, 4)) return 0;
+    int64_t rl = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t w = bd_rd32(cig + 4ull * j), op = w & 0xfu;
+        d->cigar[d->nw + j] = w;
+        if (!(flag & 4) && (op == 0 || op == 2 || op == 3 || op == 7 || op == 8)) rl += w >> 4;
+    }
+    d->tid[d->nr] = tid;
+    d->pos[d->nr] = pos;
+    d->endpos[d->nr] = (int32_t)(pos + (rl ? rl : 1));   /* htslib bam_endpos */
+    d->clip[d->nr] = clip;
+    d->cig_off[d->nr] = d->nw;
+    d->nr++;
+    d->nw += n;
+    d->st.reads++;
+    d->st.cigar_ops += n;
+    return 1;
+}
+
+svt_status svt_bam_dec_open(svt_ctx *c, int32_t n_targets, svt_bam_dec **out) {
+    if (!c || !out || n_targets < 0) return SVT_EINVAL;
+    svt_bam_dec *d = (svt_bam_dec *)calloc(1, sizeof *d);
+    if (!d) return fail(c, SVT_ENOMEM, "out of host memory");
+    d->c = c;
+    d->n_ref = n_targets;
+    d->first = 1;
+    *out = d;
+    return SVT_OK;
+}
+
+svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *b, size_t n,
+                            uint64_t skip) {
+    if (!d) return SVT_EINVAL;
+    svt_ctx *c = d->c;
+    uint64_t U = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (b[i].clen > 65536u || b[i].ulen > 65536u || b[i].coff > comp_bytes || b[i].clen > comp_bytes - b[i].coff)
+            return fail(c, SVT_EINVAL, "BGZF block outside its buffers (or over 64 KiB)");
+        if (b[i].uoff + b[i].ulen > U) U = b[i].uoff + b[i].ulen;
+    }
+    if (!bd_grow((void **)&d->buf, &d->cap, d->n + U + 1, 1)) return fail(c, SVT_ENOMEM, "out of host memory");
+    const uint32_t bad = cpu_inflate(comp, b, n, d->buf + d->n);
+    if (bad != 0xffffffffu) return fail(c, SVT_EINVAL, "corrupt BGZF block %u of the batch (does not inflate to its ISIZE)", bad);
+    size_t N = d->n + U, p = d->first ? (size_t)skip : 0;
+    if (p > N) return fail(c, SVT_EINVAL, "BAM decode: the header runs past the first batch");
+    while (p + 4 <= N) {   /* the record chain: block_size hops */
+        const uint32_t bs = bd_rd32(d->buf + p);
+        if (bs < 32) return fail(c, SVT_EINVAL, "corrupt BAM record (block_size < 32)");
+        if (p + 4 + bs > N) break;
+        if (!bd_take(d, d->buf + p + 4, bs)) return fail(c, SVT_EINVAL, "corrupt BAM record");
+        p += 4 + (size_t)bs;
+    }
+    memmove(d->buf, d->buf + p, N - p);
+    d->n = N - p;
+    d->first = 0;
+    d->st.batches++;
+    d->st.inflated_bytes += U;
+    return SVT_OK;
+}
+
+svt_status svt_bam_dec_stats_get(const svt_bam_dec *d, svt_bam_dec_stats *out) {
+    if (!d || !out) return SVT_EINVAL;
+    *out = d->st;
+    return SVT_OK;
+}
+
+static const svt_bam_dec *bd_sort_ctx;
+static int bd_cmp(const void *a, const void *b) {   /* by (tid, pos), then input order (stable) */
+    const size_t x = *(const size_t *)a, y = *(const size_t *)b;
+    const svt_bam_dec *d = bd_sort_ctx;
+    if (d->tid[x] != d->tid[y]) return d->tid[x] < d->tid[y] ? -1 : 1;
+    if (d->pos[x] != d->pos[y]) return d->pos[x] < d->pos[y] ? -1 : 1;
+    return x < y ? -1 : x > y;
+}
+
+svt_status svt_bam_dec_load(svt_bam_dec *d) {
+    if (!d) return SVT_EINVAL;
+    svt_ctx *c = d->c;
+    if (d->n) return fail(c, SVT_EINVAL, "truncated BAM record at end of file");
+    const size_t nr = d->nr;
+    size_t *idx = (size_t *)malloc(sizeof(size_t) * (nr ? nr : 1));
+    int64_t *toff = (int64_t *)calloc((size_t)d->n_ref + 1, sizeof(int64_t));
+    int32_t *pos = (int32_t *)malloc(sizeof(int32_t) * (nr ? nr : 1)), *end = (int32_t *)malloc(sizeof(int32_t) * (nr ? nr : 1));
+    uint8_t *clip = (uint8_t *)malloc(nr ? nr : 1);
+    uint64_t *off = (uint64_t *)malloc(sizeof(uint64_t) * (nr + 1));
+    uint32_t *cig = (uint32_t *)malloc(4 * (d->nw ? d->nw : 1));
+    svt_status s = SVT_ENOMEM;
+    if (idx && toff && pos && end && clip && off && cig) {
+        for (size_t i = 0; i < nr; i++) idx[i] = i;
+        bd_sort_ctx = d;
+        qsort(idx, nr, sizeof(size_t), bd_cmp);   /* the host ingest's order: sorted by (tid, pos), stable */
+        uint64_t w = 0;
+        for (size_t k = 0; k < nr; k++) {
+            const size_t i = idx[k];
+            const uint64_t o = d->cig_off[i], m = (i + 1 < nr ? d->cig_off[i + 1] : d->nw) - o;
+            pos[k] = d->pos[i]; end[k] = d->endpos[i]; clip[k] = d->clip[i];
+            off[k] = w;
+            if (m) memcpy(cig + w, d->cigar + o, 4 * m);
+            w += m;
+            toff[d->tid[i] + 1]++;
+        }
+        off[nr] = w;
+        for (int32_t t = 0; t < d->n_ref; t++) toff[t + 1] += toff[t];
+        svt_pileup_view v = {d->n_ref, toff, pos, end, off, cig, clip};
+        s = svt_load_pileup(c, &v);
+    } else {
+        fail(c, SVT_ENOMEM, "out of host memory");
+    }
+    free(idx); free(toff); free(pos); free(end); free(clip); free(off); free(cig);
+    return s;
+}
+
+void svt_bam_dec_close(svt_bam_dec *d) {
+    if (!d) return;
+    free(d->buf); free(d->tid); free(d->pos); free(d->endpos); free(d->clip); free(d->cig_off); free(d->cigar);
+    free(d);
+}

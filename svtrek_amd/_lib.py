@@ -102,6 +102,11 @@ class SvtLoadStats(C.Structure):
     ]
 
 
+class SvtBamDecStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("records", "reads", "cigar_ops", "cg_restored", "batches", "rechained",
+                                          "inflated_bytes")] + [("feed_ms", C.c_double)]
+
+
 # every symbol include/svtrek_gpu.h declares
 ENGINE_SYMBOLS = (
     "svt_open", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
@@ -112,6 +117,7 @@ ENGINE_SYMBOLS = (
     "svt_refine_device_records", "svt_reindex",
     "svt_bgzf_inflate", "svt_bgzf_inflate_device", "svt_bgzf_inflate_status", "svt_bgzf_last_inflate_ms",
     "svt_host_alloc", "svt_host_free",
+    "svt_bam_dec_open", "svt_bam_dec_feed", "svt_bam_dec_load", "svt_bam_dec_stats_get", "svt_bam_dec_close",
 )
 
 _engine = None
@@ -186,6 +192,14 @@ def bind_abi(lib: C.CDLL) -> C.CDLL:
     lib.svt_host_alloc.restype = P
     lib.svt_host_free.argtypes = [P, P]
     lib.svt_host_free.restype = None
+    lib.svt_bam_dec_open.argtypes = [P, C.c_int32, C.POINTER(P)]
+    lib.svt_bam_dec_feed.argtypes = [P, P, C.c_size_t, P, C.c_size_t, C.c_uint64]
+    lib.svt_bam_dec_load.argtypes = [P]
+    lib.svt_bam_dec_stats_get.argtypes = [P, C.POINTER(SvtBamDecStats)]
+    lib.svt_bam_dec_close.argtypes = [P]
+    lib.svt_bam_dec_close.restype = None
+    for name in ("svt_bam_dec_open", "svt_bam_dec_feed", "svt_bam_dec_load", "svt_bam_dec_stats_get"):
+        getattr(lib, name).restype = C.c_int32
     for name in ("svt_bgzf_inflate", "svt_bgzf_inflate_device", "svt_bgzf_inflate_status",
                  "svt_open", "svt_open_multi", "svt_refine_device_records", "svt_load_pileup", "svt_refine_batch", "svt_refine_device", "svt_sync",
                  "svt_reindex", "svt_count_work", "svt_sliding_window_ins", "svt_load_insseq", "svt_poa_consensus"):

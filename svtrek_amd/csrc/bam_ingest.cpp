@@ -32,10 +32,11 @@
 #include <vector>
 
 #include "svtrek_host.h"
+#include "svt_bamrec.h"
 
 namespace {
 
-constexpr uint32_t OP_M = 0, OP_D = 2, OP_N = 3, OP_S = 4, OP_EQ = 7, OP_X = 8;
+
 
 inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
@@ -470,100 +471,6 @@ struct BaiLinear {
     }
 };
 
-// htslib bam_tag2cigar's conditions: n_cigar > 0, tid >= 0, pos >= 0, cigar[0] == <l_seq>S,
-// a CG tag of type B,I (or B,i) with at least n_cigar elements and fewer than 2^29.
-bool find_cg(const uint8_t *aux, const uint8_t *end, const uint8_t **arr, uint32_t *cnt) {
-    const uint8_t *p = aux;
-    while (p + 3 <= end) {
-        char t0 = (char)p[0], t1 = (char)p[1], ty = (char)p[2];
-        p += 3;
-        size_t sz = 0;
-        switch (ty) {
-        case 'A': case 'c': case 'C': sz = 1; break;
-        case 's': case 'S': sz = 2; break;
-        case 'i': case 'I': case 'f': sz = 4; break;
-        case 'Z': case 'H': {
-            const uint8_t *q = p;
-            while (q < end && *q) q++;
-            if (q >= end) return false;
-            p = q + 1;
-            continue;
-        }
-        case 'B': {
-            if (p + 5 > end) return false;
-            char sub = (char)p[0];
-            uint32_t n = rd32(p + 1);
-            size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2
-                        : (sub == 'i' || sub == 'I' || sub == 'f') ? 4 : 0;
-            if (!es) return false;
-            if (t0 == 'C' && t1 == 'G') {
-                if (sub != 'I' && sub != 'i') return false;
-                if (p + 5 + (size_t)n * 4 > end) return false;
-                *arr = p + 5;
-                *cnt = n;
-                return true;
-            }
-            p += 5 + (size_t)n * es;
-            continue;
-        }
-        default:
-            return false;
-        }
-        p += sz;
-    }
-    return false;
-}
-
-// Where one record's CIGAR lives (after CG restoration) and its soft-clip test bits.
-struct RecView {
-    const uint8_t *cig;
-    uint32_t n;
-    bool cg;
-    bool ok;
-    int32_t tid, pos;
-    uint16_t flag;
-    uint8_t clip;
-};
-
-RecView view_record(const uint8_t *r, uint32_t bs, int32_t n_ref) {
-    RecView v{};
-    const uint8_t *rend = r + bs;
-    v.tid = (int32_t)rd32(r);
-    v.pos = (int32_t)rd32(r + 4);
-    const uint32_t l_qname = r[8];
-    const uint16_t n_cig = rd16(r + 12);
-    v.flag = rd16(r + 14);
-    const int32_t l_seq = (int32_t)rd32(r + 16);
-    v.ok = v.tid >= 0 && v.tid < n_ref && v.pos >= 0;   // only these can be yielded by a tid >= 0 query
-    if (!v.ok) return v;
-    const uint8_t *qn = r + 32, *cg = qn + l_qname;
-    if (cg + 4ull * n_cig > rend || l_seq < 0) { v.ok = false; v.n = 0xffffffffu; return v; }
-    const uint8_t *after = cg + 4ull * n_cig;   // SEQ starts here
-    const uint8_t *aux = after + (size_t)(l_seq + 1) / 2 + (size_t)l_seq;
-    v.cig = cg;
-    v.n = n_cig;
-    if (n_cig > 0 && (rd32(cg) & 0xfu) == OP_S && (int64_t)(rd32(cg) >> 4) == l_seq && aux <= rend) {
-        const uint8_t *arr;
-        uint32_t cnt;
-        if (find_cg(aux, rend, &arr, &cnt) && cnt >= n_cig && cnt < (1u << 29)) { v.cig = arr; v.n = cnt; v.cg = true; }
-    }
-    // Soft-clip test words as the reference reads them through bam1_t.data: the qname is
-    // padded with NULs to a multiple of 4 (htslib l_extranul), so cigar[-1] is the last 4
-    // bytes of the padded name and cigar[0] of an empty CIGAR is the first SEQ byte.
-    uint8_t c = 0;
-    if (v.n) {
-        if ((rd32(v.cig + 4ull * (v.n - 1)) & 0xfu) == OP_S) c |= SVT_CLIP_LAST_S;
-        if ((rd32(v.cig) & 0xfu) == OP_S) c |= SVT_CLIP_FIRST_S;
-    } else {
-        uint32_t padded = (l_qname + 3u) & ~3u;
-        uint8_t lastw0 = (padded >= 4 && padded - 4 < l_qname) ? qn[padded - 4] : 0;
-        if ((lastw0 & 0xfu) == OP_S) c |= SVT_CLIP_LAST_S;
-        if (after < rend && (after[0] & 0xfu) == OP_S) c |= SVT_CLIP_FIRST_S;
-    }
-    v.clip = c;
-    return v;
-}
-
 // Growable array without value-initialisation; large blocks grow by realloc (mremap on
 // glibc), so appending a chunk never re-copies or zero-fills what is already there.
 template <typename T>
@@ -694,7 +601,7 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
     uint64_t narena = 0;
     std::vector<size_t> roff;
     std::vector<uint32_t> rlen;
-    std::vector<RecView> views;
+    std::vector<bamrec::View> views;
     while (!done) {
         if (buf.size() - at < 4 && !need(4)) break;   // clean EOF
         // sequential boundary scan over the complete records in the buffer
@@ -716,7 +623,7 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
         views.resize(nr);
         parallel_for(rd.threads, nr, [&](size_t i0, size_t i1) {
             for (size_t i = i0; i < i1; i++)
-                views[i] = view_record(buf.data() + roff[i], rd32(buf.data() + roff[i] - 4), n_ref);
+                views[i] = bamrec::view(buf.data() + roff[i], rd32(buf.data() + roff[i] - 4), n_ref);
         });
         if (region)   // sorted file: the first record past (tid1, end1) ends the read
             for (size_t i = 0; i < nr; i++) {
@@ -732,7 +639,7 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
         const size_t base = b->pos.size();
         size_t kept = 0;
         for (size_t i = 0; i < nr; i++) {
-            if (views[i].n == 0xffffffffu) return bail("corrupt BAM record");
+            if (views[i].bad) return bail("corrupt BAM record");
             if (views[i].ok) kept++;
             if (views[i].cg) b->n_cg++;
         }
@@ -748,20 +655,14 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
             return bail("out of host memory");
         parallel_for(rd.threads, nr, [&](size_t i0, size_t i1) {
             for (size_t i = i0; i < i1; i++) {
-                const RecView &v = views[i];
+                const bamrec::View &v = views[i];
                 if (!v.ok) continue;
                 const size_t k = slot[i];
                 uint32_t *dst = b->cigar.data() + narena + off[i];
                 if (v.n) memcpy(dst, v.cig, 4ull * v.n);
-                int64_t rl = 0;
-                if (!(v.flag & 4))
-                    for (uint32_t j = 0; j < v.n; j++) {
-                        const uint32_t op = dst[j] & 0xfu;
-                        if (op == OP_M || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X) rl += dst[j] >> 4;
-                    }
                 b->pos[k] = v.pos;
-                b->endpos[k] = (int32_t)(v.pos + (rl ? rl : 1));   // htslib bam_endpos
-                b->clip[k] = v.clip;
+                b->endpos[k] = bamrec::endpos(v);   // htslib bam_endpos
+                b->clip[k] = (uint8_t)v.clip;
                 b->cig_off[k] = narena + off[i];
                 tid_of[k] = v.tid;
             }
@@ -812,6 +713,103 @@ svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t 
     for (size_t k = 0; k < n; k++) b->tid_off[(size_t)tid_of[k] + 1]++;
     for (int32_t t = 0; t < n_ref; t++) b->tid_off[(size_t)t + 1] += b->tid_off[(size_t)t];
     return b;
+}
+
+int svth_bam_read_device(const char *path, int threads, const svth_dev_sink *sink, int32_t *n_targets, double *stage4,
+                         char *err, size_t errcap) {
+    auto fail = [&](const std::string &m) {
+        if (err && errcap) snprintf(err, errcap, "%s", m.c_str());
+        return 1;
+    };
+    if (!sink || !sink->begin || !sink->feed) return fail("no device sink");
+    const double t_start = BgzfReader::now();
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(std::string("cannot open BAM: ") + path);
+    BgzfReader rd;
+    rd.f = f;
+    rd.threads = threads < 1 ? 1 : threads;
+    // batches of whole BGZF blocks through read_next (its input buffers from the sink's allocator)
+    svth_inflater cfg{};
+    cfg.alloc = sink->alloc;
+    cfg.release = sink->release;
+    cfg.user = sink->user;
+    cfg.batch_bytes = sink->batch_bytes;
+    rd.inf = &cfg;
+    {
+        struct stat st;
+        rd.fsize = fstat(fileno(f), &st) == 0 ? (uint64_t)st.st_size : 0;
+    }
+    auto bail = [&](const std::string &m) {
+        rd.drop_pending();
+        fclose(f);
+        return fail(rd.err.empty() ? m : rd.err);
+    };
+    BgzfReader::Comp c = rd.read_next();
+    if (!c.ok) return bail(c.err);
+    if (c.blks.empty()) return bail("not a BAM file (no BGZF blocks)");
+    // the header (magic, text, references) on the host: inflate the first blocks until it is complete
+    std::vector<uint8_t> h;
+    size_t bi = 0;
+    auto need = [&](size_t k) -> bool {
+        while (h.size() < k) {
+            if (bi >= c.blks.size()) return false;
+            const svt_bgzf_block &b = c.blks[bi++];
+            const size_t o = h.size();
+            h.resize(o + b.ulen);
+            z_stream zs;
+            memset(&zs, 0, sizeof zs);
+            if (inflateInit2(&zs, -15) != Z_OK) return false;
+            zs.next_in = rd.cins[c.i].p + b.coff;
+            zs.avail_in = (uInt)b.clen;
+            zs.next_out = h.data() + o;
+            zs.avail_out = (uInt)b.ulen;
+            const int rc = inflate(&zs, Z_FINISH);
+            inflateEnd(&zs);
+            if (rc != Z_STREAM_END || zs.total_out != b.ulen) return false;
+        }
+        return true;
+    };
+    if (!need(8) || memcmp(h.data(), "BAM\1", 4) != 0) return bail("not a BAM file");
+    size_t at = 8 + (size_t)rd32(h.data() + 4);
+    if (!need(at + 4)) return bail("truncated BAM header (or longer than one batch)");
+    const int32_t n_ref = (int32_t)rd32(h.data() + at);
+    at += 4;
+    if (n_ref < 0) return bail("bad n_ref");
+    for (int32_t i = 0; i < n_ref; i++) {
+        if (!need(at + 4)) return bail("truncated reference list (or longer than one batch)");
+        const uint32_t ln = rd32(h.data() + at);
+        at += 4 + (size_t)ln + 4;
+        if (!need(at)) return bail("truncated reference list (or longer than one batch)");
+    }
+    if (n_targets) *n_targets = n_ref;
+    char e[512] = {0};
+    if (sink->begin(sink->user, n_ref, e, sizeof e) != 0) return bail(e[0] ? e : "device sink: begin failed");
+    // the batches: the next one read and scanned by a helper thread while this one is decoded
+    double t_feed = 0, t_wait = 0;
+    uint64_t skip = at;
+    for (;;) {
+        if (!rd.eof || rd.carry_n) rd.pending_comp = std::async(std::launch::async, [&rd] { return rd.read_next(); });
+        const double t0 = BgzfReader::now();
+        const int rc = sink->feed(sink->user, rd.cins[c.i].p, c.p, c.blks.data(), c.blks.size(), skip, e, sizeof e);
+        t_feed += BgzfReader::now() - t0;
+        skip = 0;
+        if (rc != 0) return bail(e[0] ? e : "device sink: feed failed");
+        if (!rd.pending_comp.valid()) break;
+        const double t1 = BgzfReader::now();
+        c = rd.pending_comp.get();
+        t_wait += BgzfReader::now() - t1;
+        if (!c.ok) return bail(c.err);
+        if (c.blks.empty()) break;
+    }
+    rd.drop_pending();
+    fclose(f);
+    if (stage4) {
+        stage4[0] = rd.t_read;
+        stage4[1] = t_feed;
+        stage4[2] = t_wait + rd.t_alloc_r;
+        stage4[3] = BgzfReader::now() - t_start;
+    }
+    return 0;
 }
 
 void svth_bam_free(svth_bam *b) { delete b; }

@@ -40,6 +40,7 @@
 
 #include "../../include/svtrek_gpu.h"
 #include "svt_inflate.h"
+#include "svt_bamrec.h"
 
 #define SVT_VERSION "svtrek_amd 0.17.0 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
 
@@ -1687,6 +1688,7 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 #include "svt_index.inc"
 #include "svt_index2.inc"
 #include "svt_poa.inc"
+#include "svt_bam.inc"
 
 // ------------------------------------------------------------------ BGZF inflate
 // One lane per BGZF block (svt_inflate.h): a BAM's blocks are independent DEFLATE streams of
@@ -2289,54 +2291,42 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
 }  // namespace
 }  // extern "C++"
 
-static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
-    if (!c || !p) return SVT_EINVAL;
-    if (p->n_targets < 0 || (p->n_targets > 0 && !p->tid_off))
-        return fail(c, SVT_EINVAL, "pileup: %s", "bad n_targets / tid_off");
-    DEV_GUARD(c);
-    free_pileup(c);
+// The pileup of a context from per-read columns in host memory -- nc[r] = n_cigar | clip << 30,
+// soff[0..nr] the reads' offsets in the CIGAR stream (a read without ops owns one 0M word) --
+// and the stream itself, in host memory (stream_h) or already on the device (stream_d, with
+// STREAM_PAD zero words after its end: adopted, the context frees it).  The host pass
+// validates and builds the prefix-max endpos, the records, the read buckets, the index ranges;
+// then the uploads and the first device index build.
+static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, const int32_t *pos, const int32_t *endpos,
+                            const uint32_t *nc, const uint64_t *soff, const uint32_t *stream_h, uint32_t *stream_d,
+                            uint64_t nops, double t_pre_ms) {
     using clk = std::chrono::steady_clock;
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     const clk::time_point t_start = clk::now();
-    c->load_stats = svt_load_stats{};
-    const int32_t nt = p->n_targets;
-    const int64_t nr = nt ? p->tid_off[nt] : 0;
-    if (nt && p->tid_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "tid_off[0] != 0");
-    for (int32_t t = 0; t < nt; t++)
-        if (p->tid_off[t + 1] < p->tid_off[t]) return fail(c, SVT_EINVAL, "pileup: %s", "tid_off not monotone");
-    if (nr > 0 && (!p->pos || !p->endpos || !p->cig_off || (!p->cigar && p->cig_off[nr] > 0)))
-        return fail(c, SVT_EINVAL, "pileup: %s", "missing arrays");
-    const uint64_t nops = nr > 0 ? p->cig_off[nr] : 0;
-    if (nr > 0 && p->cig_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "cig_off[0] != 0");
-
+    const int64_t nr = nt ? tid_off[nt] : 0;
+    const uint64_t nstream = nr > 0 ? soff[nr] : 0;
     // ---- host pass, per contig in parallel: validation, prefix-max endpos, records, buckets
     std::vector<int32_t> emax((size_t)nr);
     std::vector<uint4> rec((size_t)nr);
     std::vector<std::vector<uint2>> bk((size_t)nt);
-    std::vector<int64_t> zeros((size_t)nt, 0);   // reads with n_cigar == 0 per contig
     std::vector<const char *> bad((size_t)nt, nullptr);
     parallel_for((size_t)nt, 16, [&](size_t t) {
-        const int64_t r0 = p->tid_off[t], r1 = p->tid_off[t + 1];
+        const int64_t r0 = tid_off[t], r1 = tid_off[t + 1];
         if (r1 - r0 > 0xffffffffll) { bad[t] = "> 2^32 reads on one contig"; return; }
         int32_t m = INT32_MIN, maxpos = 0;
-        int64_t z = 0;
         for (int64_t r = r0; r < r1; r++) {
-            if (r > r0 && p->pos[r] < p->pos[r - 1]) { bad[t] = "reads not sorted by pos within a contig"; return; }
-            if (p->pos[r] < 0 || p->endpos[r] <= p->pos[r]) { bad[t] = "pos < 0 or endpos <= pos"; return; }
-            const uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
-            if (o1 < o0 || o1 > nops || o1 - o0 > NCIG_MASK) { bad[t] = "bad cig_off"; return; }
-            const uint32_t ncig = (uint32_t)(o1 - o0);
-            uint32_t clip;
-            if (p->clip) clip = p->clip[r] & 3u;
-            else clip = ncig ? (((p->cigar[o1 - 1] & 0xfu) == OP_SOFT ? 1u : 0u) |
-                                ((p->cigar[o0] & 0xfu) == OP_SOFT ? 2u : 0u)) : 0u;
-            z += ncig == 0;
-            if (p->endpos[r] > m) m = p->endpos[r];
-            maxpos = std::max(maxpos, p->pos[r]);
+            if (r > r0 && pos[r] < pos[r - 1]) { bad[t] = "reads not sorted by pos within a contig"; return; }
+            if (pos[r] < 0 || endpos[r] <= pos[r]) { bad[t] = "pos < 0 or endpos <= pos"; return; }
+            const uint64_t w = soff[r + 1] - soff[r], n = nc[r] & NCIG_MASK;
+            if (soff[r + 1] < soff[r] || soff[r + 1] > nstream || w != std::max<uint64_t>(n, 1)) {
+                bad[t] = "bad cig_off";
+                return;
+            }
+            if (endpos[r] > m) m = endpos[r];
+            maxpos = std::max(maxpos, pos[r]);
             emax[(size_t)r] = m;
-            rec[(size_t)r] = make_uint4((uint32_t)p->pos[r], (uint32_t)p->endpos[r], ncig | (clip << 30), 0u);
+            rec[(size_t)r] = make_uint4((uint32_t)pos[r], (uint32_t)endpos[r], nc[r], 0u);
         }
-        zeros[t] = z;
         // bucket b = 0..nb-1: {first contig-relative read with pos >= b << BKT_SHIFT, first with
         // emax >= b << BKT_SHIFT}; the last bucket lies past every pos and endpos: {nr, nr}
         const int64_t top = r1 > r0 ? std::max<int64_t>(maxpos, m) : 0;
@@ -2346,44 +2336,23 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         int64_t rp = r0, re = r0;
         for (int64_t b = 0; b < nb; b++) {
             const int64_t x = b << BKT_SHIFT;
-            while (rp < r1 && (int64_t)p->pos[rp] < x) rp++;
+            while (rp < r1 && (int64_t)pos[rp] < x) rp++;
             while (re < r1 && (int64_t)emax[(size_t)re] < x) re++;
             B.push_back(make_uint2((uint32_t)(rp - r0), (uint32_t)(re - r0)));
         }
     });
     for (int32_t t = 0; t < nt; t++)
         if (bad[(size_t)t]) return fail(c, SVT_EINVAL, "pileup: %s", bad[(size_t)t]);
+    if (stream_d) c->d_cigar = stream_d;   // the context owns it from here on (freed with the pileup)
     std::vector<int64_t> bkt_off((size_t)nt + 1, 0);
     for (int32_t t = 0; t < nt; t++) bkt_off[(size_t)t + 1] = bkt_off[(size_t)t] + (int64_t)bk[(size_t)t].size();
     std::vector<uint2> bkt((size_t)bkt_off[(size_t)nt]);
     parallel_for((size_t)nt, 16, [&](size_t t) { std::copy(bk[t].begin(), bk[t].end(), bkt.begin() + bkt_off[t]); });
-    // ---- the CIGAR stream: the caller's words; a read with n_cigar == 0 gets one 0M word (no
-    // advance, never a candidate) so that every read owns a stream op (svt_index.inc)
-    int64_t nzero = 0;
-    for (int32_t t = 0; t < nt; t++) nzero += zeros[(size_t)t];
-    const uint64_t *soff = p->cig_off;
-    const uint32_t *strm = p->cigar;
-    std::vector<uint64_t> soff2;
-    std::vector<uint32_t> strm2;
-    if (nzero > 0) {
-        soff2.resize((size_t)nr + 1);
-        strm2.reserve(nops + (uint64_t)nzero);
-        for (int64_t r = 0; r < nr; r++) {
-            soff2[(size_t)r] = strm2.size();
-            const uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
-            if (o1 == o0) strm2.push_back(0u);
-            else strm2.insert(strm2.end(), p->cigar + o0, p->cigar + o1);
-        }
-        soff2[(size_t)nr] = strm2.size();
-        soff = soff2.data();
-        strm = strm2.data();
-    }
-    const uint64_t nstream = nr > 0 ? soff[nr] : 0;
     // ---- ranges of the index build: ~T stream ops each, cut at read starts and contig starts
     const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / c->ix_ranges, 2048), 1ull << 26);
     std::vector<std::vector<uint64_t>> pt((size_t)nt);
     parallel_for((size_t)nt, 16, [&](size_t t) {
-        for (int64_t r = p->tid_off[t], r1 = p->tid_off[t + 1]; r < r1;) {
+        for (int64_t r = tid_off[t], r1 = tid_off[t + 1]; r < r1;) {
             pt[t].push_back((uint64_t)r);
             const uint64_t s0 = soff[r];
             for (r++; r < r1 && soff[r] - s0 < T; r++) {}
@@ -2399,19 +2368,20 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
     c->n_groups = (uint32_t)((nr + WAVE - 1) / WAVE);
     for (int64_t g0 = 0; g0 < nr && c->n_groups; g0 += WAVE)
         if (soff[std::min<int64_t>(g0 + WAVE, nr)] - soff[g0] >= (1ull << 27)) c->n_groups = 0;
-    c->load_stats.host_ms = ms_since(t_start);
+    c->load_stats.host_ms = t_pre_ms + ms_since(t_start);
 
     const clk::time_point t_up = clk::now();
     svt_status s;
-    if ((s = upload(c, c->d_pos, p->pos, (size_t)nr))) return s;
+    if ((s = upload(c, c->d_pos, pos, (size_t)nr))) return s;
     if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
     if ((s = upload(c, c->d_rec, rec.data(), (size_t)nr))) return s;
     if ((s = upload(c, c->d_off64, soff, nr > 0 ? (size_t)nr + 1 : 0, nr > 0 ? 0 : 1))) return s;
     if ((s = upload(c, c->d_bkt, bkt.data(), bkt.size()))) return s;
     if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
-    if (nt > 0) { if ((s = upload(c, c->d_tid_off, p->tid_off, (size_t)nt + 1))) return s; }
+    if (nt > 0) { if ((s = upload(c, c->d_tid_off, tid_off, (size_t)nt + 1))) return s; }
     else if ((s = upload<int64_t>(c, c->d_tid_off, nullptr, 0, 1))) return s;
-    if ((s = upload(c, c->d_cigar, strm, (size_t)nstream, STREAM_PAD))) return s;
+    if (stream_d) c->dev_bytes += (nstream + STREAM_PAD) * 4u;
+    else if ((s = upload(c, c->d_cigar, stream_h, (size_t)nstream, STREAM_PAD))) return s;
     if ((s = upload(c, c->d_part, part.data(), part.size()))) return s;
     const size_t S = (size_t)nr + 1;
     if ((s = upload<uint64_t>(c, c->d_spoffD, nullptr, 0, S))) return s;
@@ -2462,8 +2432,71 @@ static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
         }
     }
     c->loaded = true;
-    c->load_stats.total_ms = ms_since(t_start);
     return SVT_OK;
+}
+
+static svt_status load_1(svt_ctx *c, const svt_pileup_view *p) {
+    if (!c || !p) return SVT_EINVAL;
+    if (p->n_targets < 0 || (p->n_targets > 0 && !p->tid_off))
+        return fail(c, SVT_EINVAL, "pileup: %s", "bad n_targets / tid_off");
+    DEV_GUARD(c);
+    free_pileup(c);
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t_start = clk::now();
+    c->load_stats = svt_load_stats{};
+    const int32_t nt = p->n_targets;
+    const int64_t nr = nt ? p->tid_off[nt] : 0;
+    if (nt && p->tid_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "tid_off[0] != 0");
+    for (int32_t t = 0; t < nt; t++)
+        if (p->tid_off[t + 1] < p->tid_off[t]) return fail(c, SVT_EINVAL, "pileup: %s", "tid_off not monotone");
+    if (nr > 0 && (!p->pos || !p->endpos || !p->cig_off || (!p->cigar && p->cig_off[nr] > 0)))
+        return fail(c, SVT_EINVAL, "pileup: %s", "missing arrays");
+    const uint64_t nops = nr > 0 ? p->cig_off[nr] : 0;
+    if (nr > 0 && p->cig_off[0] != 0) return fail(c, SVT_EINVAL, "pileup: %s", "cig_off[0] != 0");
+    // per read n_cigar | clip << 30 (clip from the caller, or from the CIGAR words)
+    std::vector<uint32_t> nc((size_t)nr);
+    std::vector<int64_t> zeros((size_t)std::max(nt, 1), 0);   // reads with n_cigar == 0 per contig
+    std::vector<const char *> bad((size_t)std::max(nt, 1), nullptr);
+    parallel_for((size_t)nt, 16, [&](size_t t) {
+        for (int64_t r = p->tid_off[t], r1 = p->tid_off[t + 1]; r < r1; r++) {
+            const uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
+            if (o1 < o0 || o1 > nops || o1 - o0 > NCIG_MASK) { bad[t] = "bad cig_off"; return; }
+            const uint32_t ncig = (uint32_t)(o1 - o0);
+            uint32_t clip;
+            if (p->clip) clip = p->clip[r] & 3u;
+            else clip = ncig ? (((p->cigar[o1 - 1] & 0xfu) == OP_SOFT ? 1u : 0u) |
+                                ((p->cigar[o0] & 0xfu) == OP_SOFT ? 2u : 0u)) : 0u;
+            zeros[t] += ncig == 0;
+            nc[(size_t)r] = ncig | clip << 30;
+        }
+    });
+    for (int32_t t = 0; t < nt; t++)
+        if (bad[(size_t)t]) return fail(c, SVT_EINVAL, "pileup: %s", bad[(size_t)t]);
+    // ---- the CIGAR stream: the caller's words; a read with n_cigar == 0 gets one 0M word (no
+    // advance, never a candidate) so that every read owns a stream op (svt_index.inc)
+    int64_t nzero = 0;
+    for (int32_t t = 0; t < nt; t++) nzero += zeros[(size_t)t];
+    const uint64_t *soff = p->cig_off;
+    const uint32_t *strm = p->cigar;
+    std::vector<uint64_t> soff2;
+    std::vector<uint32_t> strm2;
+    if (nzero > 0) {
+        soff2.resize((size_t)nr + 1);
+        strm2.reserve(nops + (uint64_t)nzero);
+        for (int64_t r = 0; r < nr; r++) {
+            soff2[(size_t)r] = strm2.size();
+            const uint64_t o0 = p->cig_off[r], o1 = p->cig_off[r + 1];
+            if (o1 == o0) strm2.push_back(0u);
+            else strm2.insert(strm2.end(), p->cigar + o0, p->cigar + o1);
+        }
+        soff2[(size_t)nr] = strm2.size();
+        soff = soff2.data();
+        strm = strm2.data();
+    }
+    const double pre = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
+    svt_status s = load_core(c, nt, p->tid_off, p->pos, p->endpos, nc.data(), soff, strm, nullptr, nops, pre);
+    c->load_stats.total_ms = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
+    return s;
 }
 
 // svt_open_multi: run fn(ctx_d, lo_d, hi_d) for the contiguous slices [lo_d, hi_d) of n items,
@@ -2862,6 +2895,306 @@ void svt_host_free(svt_ctx *c, void *p) {
     if (!c || !p) return;
     DevGuard dg(c->device);
     (void)hipHostFree(p);
+}
+
+// ---- BAM records decoded on the device (svt_bam.inc)
+}  // extern "C"
+
+struct svt_bam_dec {
+    svt_ctx *c = nullptr;
+    int32_t n_ref = 0;
+    hipStream_t st = nullptr;
+    uint8_t *d_comp = nullptr;
+    size_t comp_cap = 0;
+    svt_bgzf_block *d_blk = nullptr;
+    size_t blk_cap = 0;
+    uint8_t *d_buf[2] = {nullptr, nullptr};   // inflated batches: [carried tail | this batch]
+    size_t buf_cap[2] = {0, 0};
+    int cur = 0;
+    uint64_t tail = 0;                        // bytes of the incomplete record at the front of d_buf[cur]
+    bool first = true;
+    BdChunk *d_ch = nullptr;
+    uint32_t *d_base = nullptr;
+    size_t ch_cap = 0, base_cap = 0;
+    BdRec *d_rec = nullptr;
+    BdTot *d_pre = nullptr;
+    size_t rec_cap = 0, pre_cap = 0;
+    BdCheck *d_chk = nullptr;
+    void *d_tmp = nullptr;
+    size_t tmp_cap = 0;
+    BdCols cols{};
+    uint64_t col_cap = 0, word_cap = 0;       // capacities of the columns (reads) and the stream (words)
+    uint64_t nkept = 0, nwords = 0;
+    svt_bam_dec_stats stats{};
+};
+
+namespace {
+template <typename T>
+svt_status bd_grow(svt_ctx *c, T *&p, size_t &cap, size_t need, size_t keep = 0) {   // device, keeping `keep` elements
+    if (need <= cap) return SVT_OK;
+    const size_t nc = std::max(need, cap + cap / 2);
+    T *q = nullptr;
+    if (hipMalloc(&q, nc * sizeof(T)) != hipSuccess) return fail(c, SVT_ENOMEM, "%s", "device memory for the BAM decode");
+    if (keep && p) HIP_TRY(c, hipMemcpy(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice));
+    hfree(p);
+    p = q;
+    cap = nc;
+    return SVT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+svt_status svt_bam_dec_open(svt_ctx *c, int32_t n_targets, svt_bam_dec **out) {
+    if (!c || !out || n_targets < 0) return SVT_EINVAL;
+    *out = nullptr;
+    DEV_GUARD(c);
+    svt_bam_dec *d = new (std::nothrow) svt_bam_dec();
+    if (!d) return fail(c, SVT_ENOMEM, "%s", "host memory");
+    d->c = c;
+    d->n_ref = n_targets;
+    if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&d->d_chk, sizeof(BdCheck)) != hipSuccess) {
+        svt_bam_dec_close(d);
+        return fail(c, SVT_EDEVICE, "%s", "BAM decode: stream / buffers");
+    }
+    if (!c->d_infs && hipMalloc(&c->d_infs, (size_t)INF_GRID * WAVE * sizeof(InfSlow)) != hipSuccess) {
+        svt_bam_dec_close(d);
+        return fail(c, SVT_ENOMEM, "%s", "inflate scratch");
+    }
+    if (!c->d_inferr && hipMalloc(&c->d_inferr, sizeof(uint32_t)) != hipSuccess) {
+        svt_bam_dec_close(d);
+        return fail(c, SVT_ENOMEM, "%s", "inflate scratch");
+    }
+    *out = d;
+    return SVT_OK;
+}
+
+svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
+                            size_t n, uint64_t skip) {
+    if (!d) return SVT_EINVAL;
+    svt_ctx *c = d->c;
+    if (n && (!comp || !blocks)) return fail(c, SVT_EINVAL, "%s", "null buffer");
+    if (n > 0xfffffffeull) return fail(c, SVT_EINVAL, "%s", "more than 2^32 - 2 blocks in one call");
+    uint64_t U = 0;
+    for (size_t i = 0; i < n; i++) {   // every block inside its buffers (the kernel trusts the table)
+        const svt_bgzf_block &k = blocks[i];
+        if (k.clen > 65536u || k.ulen > 65536u || k.coff > comp_bytes || k.clen > comp_bytes - k.coff)
+            return fail(c, SVT_EINVAL, "%s", "BGZF block outside its buffers (or over 64 KiB)");
+        U = std::max<uint64_t>(U, k.uoff + k.ulen);
+    }
+    DEV_GUARD(c);
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    svt_status s;
+    const uint64_t T = d->tail, N = T + U;
+    const uint64_t r0 = d->first ? skip : 0;
+    if (r0 > N) return fail(c, SVT_EINVAL, "%s", "BAM decode: the header runs past the first batch");
+    if ((s = bd_grow(c, d->d_comp, d->comp_cap, comp_bytes + 64)) || (s = bd_grow(c, d->d_blk, d->blk_cap, std::max<size_t>(n, 1))) ||
+        (s = bd_grow(c, d->d_buf[d->cur], d->buf_cap[d->cur], N + 64, T)))
+        return s;
+    uint8_t *buf = d->d_buf[d->cur];
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(d->d_comp, comp, comp_bytes, hipMemcpyHostToDevice, d->st));
+        HIP_TRY(c, hipMemcpyAsync(d->d_blk, blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->st));
+        HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), d->st));
+        const unsigned grid = (unsigned)std::min<size_t>((n + WAVE - 1) / WAVE, (size_t)INF_GRID);
+        hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, d->st, d->d_comp, d->d_blk, (uint32_t)n, buf + T,
+                           c->d_infs, c->d_inferr);
+        HIP_TRY(c, hipGetLastError());
+    }
+    const uint64_t span = N - r0;
+    const uint32_t nch = (uint32_t)((span + BD_CHUNK - 1) / BD_CHUNK);
+    BdCheck chk{1u, 0u, 0ull, N, 0u, 0u};
+    if (nch) {
+        if ((s = bd_grow(c, d->d_ch, d->ch_cap, nch)) || (s = bd_grow(c, d->d_base, d->base_cap, nch))) return s;
+        hipLaunchKernelGGL(bd_chunk_kernel, dim3(nch), dim3(WAVE), 0, d->st, buf, r0, N, nch, d->n_ref, d->d_ch);
+        hipLaunchKernelGGL(bd_check_kernel, dim3(1), dim3(WAVE), 0, d->st, buf, d->d_ch, nch, r0, N, d->d_chk);
+        HIP_TRY(c, hipGetLastError());
+        uint32_t ierr = 0xffffffffu;
+        HIP_TRY(c, hipMemcpyAsync(&chk, d->d_chk, sizeof chk, hipMemcpyDeviceToHost, d->st));
+        HIP_TRY(c, hipMemcpyAsync(&ierr, c->d_inferr, sizeof ierr, hipMemcpyDeviceToHost, d->st));
+        HIP_TRY(c, hipStreamSynchronize(d->st));
+        if (n && ierr != 0xffffffffu) {
+            char m[64];
+            snprintf(m, sizeof m, "%u", ierr);
+            return fail(c, SVT_EINVAL, "corrupt BGZF block %s of the batch (does not inflate to its ISIZE)", m);
+        }
+        if (!chk.ok) {   // a wrong guess: the exact chain, hop by hop
+            d->stats.rechained++;
+            hipLaunchKernelGGL(bd_chain_kernel, dim3(1), dim3(WAVE), 0, d->st, buf, r0, N, nch, d->d_ch);
+            hipLaunchKernelGGL(bd_check_kernel, dim3(1), dim3(WAVE), 0, d->st, buf, d->d_ch, nch, r0, N, d->d_chk);
+            HIP_TRY(c, hipGetLastError());
+            HIP_TRY(c, hipMemcpyAsync(&chk, d->d_chk, sizeof chk, hipMemcpyDeviceToHost, d->st));
+            HIP_TRY(c, hipStreamSynchronize(d->st));
+            if (!chk.ok) return fail(c, SVT_EDEVICE, "%s", "BAM decode: the exact record chain failed its own check");
+        }
+        if (chk.bad) return fail(c, SVT_EINVAL, "%s", "corrupt BAM record (block_size < 32)");
+    }
+    if (chk.nrec) {
+        const uint64_t nrec = chk.nrec;
+        if (nrec >= 0xffffffffull) return fail(c, SVT_EINVAL, "%s", "BAM decode: more than 2^32 records in one batch");
+        if ((s = bd_grow(c, d->d_rec, d->rec_cap, nrec)) || (s = bd_grow(c, d->d_pre, d->pre_cap, nrec))) return s;
+        // the chunks' record counts -> their first record's index; the records; their kept / word prefixes
+        const auto cnt = hipcub::TransformInputIterator<uint32_t, BdCntOf, const BdChunk *>(d->d_ch, BdCntOf());
+        const auto tot = hipcub::TransformInputIterator<BdTot, BdTotOf, const BdRec *>(d->d_rec, BdTotOf());
+        size_t need1 = 0, need2 = 0;
+        HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need1, cnt, d->d_base, (int)chk.nk, d->st));
+        HIP_TRY(c, hipcub::DeviceScan::ExclusiveScan(nullptr, need2, tot, d->d_pre, BdTotSum(), BdTot{0, 0, 0, 0, 0},
+                                                     (int)nrec, d->st));
+        if ((s = bd_grow(c, reinterpret_cast<uint8_t *&>(d->d_tmp), d->tmp_cap, std::max(need1, need2)))) return s;
+        size_t t1 = d->tmp_cap, t2 = d->tmp_cap;
+        HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(d->d_tmp, t1, cnt, d->d_base, (int)chk.nk, d->st));
+        hipLaunchKernelGGL(bd_rec_kernel, dim3(chk.nk), dim3(WAVE), 0, d->st, buf, d->d_ch, d->d_base, chk.nk, d->n_ref,
+                           d->d_rec);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipcub::DeviceScan::ExclusiveScan(d->d_tmp, t2, tot, d->d_pre, BdTotSum(), BdTot{0, 0, 0, 0, 0},
+                                                     (int)nrec, d->st));
+        BdTot last{};
+        BdRec lr{};
+        HIP_TRY(c, hipMemcpyAsync(&last, d->d_pre + nrec - 1, sizeof last, hipMemcpyDeviceToHost, d->st));
+        HIP_TRY(c, hipMemcpyAsync(&lr, d->d_rec + nrec - 1, sizeof lr, hipMemcpyDeviceToHost, d->st));
+        HIP_TRY(c, hipStreamSynchronize(d->st));
+        const BdTot all = BdTotSum()(last, BdTotOf()(lr));
+        if (all.bad) return fail(c, SVT_EINVAL, "%s", "corrupt BAM record");
+        // the columns and the stream (STREAM_PAD spare words), grown keeping what they hold
+        const uint64_t G = d->nkept + all.keep + 1, W = d->nwords + all.words + STREAM_PAD;
+        if (G > d->col_cap) {   // every column to the same capacity
+            size_t cc;
+            cc = d->col_cap; if ((s = bd_grow(c, d->cols.tid, cc, G, d->nkept))) return s;
+            cc = d->col_cap; if ((s = bd_grow(c, d->cols.pos, cc, G, d->nkept))) return s;
+            cc = d->col_cap; if ((s = bd_grow(c, d->cols.endpos, cc, G, d->nkept))) return s;
+            cc = d->col_cap; if ((s = bd_grow(c, d->cols.nc, cc, G, d->nkept))) return s;
+            cc = d->col_cap; if ((s = bd_grow(c, d->cols.soff, cc, G, d->nkept))) return s;
+            d->col_cap = cc;
+        }
+        if ((s = bd_grow(c, d->cols.stream, d->word_cap, W, d->nwords))) return s;
+        hipLaunchKernelGGL(bd_copy_kernel, dim3((unsigned)std::min<uint64_t>((nrec + 3) / 4, 16384)), dim3(256), 0, d->st,
+                           buf, d->d_rec, d->d_pre, nrec, d->cols, d->nkept, d->nwords);
+        HIP_TRY(c, hipGetLastError());
+        d->nkept += all.keep;
+        d->nwords += all.words;
+        d->stats.records += nrec;
+        d->stats.reads += all.keep;
+        d->stats.cigar_ops += all.ops;
+        d->stats.cg_restored += all.cg;
+    }
+    // the incomplete last record moves to the front of the other buffer
+    const uint64_t nt = N - chk.tail;
+    int nx = d->cur ^ 1;
+    if ((s = bd_grow(c, d->d_buf[nx], d->buf_cap[nx], std::max<uint64_t>(nt, 1) + 64))) return s;
+    if (nt) HIP_TRY(c, hipMemcpyAsync(d->d_buf[nx], buf + chk.tail, nt, hipMemcpyDeviceToDevice, d->st));
+    HIP_TRY(c, hipStreamSynchronize(d->st));
+    d->cur = nx;
+    d->tail = nt;
+    d->first = false;
+    d->stats.batches++;
+    d->stats.inflated_bytes += U;
+    d->stats.feed_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return SVT_OK;
+}
+
+svt_status svt_bam_dec_stats_get(const svt_bam_dec *d, svt_bam_dec_stats *out) {
+    if (!d || !out) return SVT_EINVAL;
+    *out = d->stats;
+    return SVT_OK;
+}
+
+svt_status svt_bam_dec_load(svt_bam_dec *d) {
+    if (!d) return SVT_EINVAL;
+    svt_ctx *c = d->c;
+    if (d->tail) return fail(c, SVT_EINVAL, "%s", "truncated BAM record at end of file");
+    DEV_GUARD(c);
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    free_pileup(c);
+    c->load_stats = svt_load_stats{};
+    const int32_t nt = d->n_ref;
+    const uint64_t n = d->nkept;
+    svt_status s;
+    // sortedness and the contig boundaries, on the device
+    int64_t *d_toff = nullptr;
+    uint32_t *d_uns = nullptr;
+    HIP_TRY(c, hipMalloc(&d_toff, ((size_t)nt + 1) * sizeof(int64_t)));
+    if (hipMalloc(&d_uns, sizeof(uint32_t)) != hipSuccess) { hfree(d_toff); return fail(c, SVT_ENOMEM, "%s", "device"); }
+    std::vector<int64_t> toff((size_t)nt + 1, 0);
+    uint32_t uns = 0;
+    hipError_t e = hipMemsetAsync(d_uns, 0, sizeof(uint32_t), d->st);
+    if (e == hipSuccess) e = hipMemsetAsync(d_toff, 0, ((size_t)nt + 1) * sizeof(int64_t), d->st);
+    if (e == hipSuccess) {
+        const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 256) / 256, 65536));
+        hipLaunchKernelGGL(bd_finish_kernel, dim3(g), dim3(256), 0, d->st, d->cols.tid, d->cols.pos, n, nt, d_toff, d_uns);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(toff.data(), d_toff, toff.size() * sizeof(int64_t), hipMemcpyDeviceToHost, d->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&uns, d_uns, sizeof uns, hipMemcpyDeviceToHost, d->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->st);
+    hfree(d_toff);
+    hfree(d_uns);
+    if (e != hipSuccess) return fail(c, SVT_EDEVICE, "BAM decode finish: %s", hipGetErrorString(e));
+    // the per-read columns the host pass reads (pos, endpos, n_cigar | clip, stream offsets)
+    std::vector<int32_t> pos(n), endpos(n), tid(uns ? n : 0);
+    std::vector<uint32_t> nc(n);
+    std::vector<uint64_t> soff(n + 1);
+    if (n) {
+        HIP_TRY(c, hipMemcpy(pos.data(), d->cols.pos, n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(endpos.data(), d->cols.endpos, n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(nc.data(), d->cols.nc, n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(soff.data(), d->cols.soff, n * 8, hipMemcpyDeviceToHost));
+        if (uns) HIP_TRY(c, hipMemcpy(tid.data(), d->cols.tid, n * 4, hipMemcpyDeviceToHost));
+    }
+    soff[n] = d->nwords;
+    const double pre = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    if (uns) {   // not coordinate-sorted: sort on the host (stable, by tid then pos), as the host ingest does
+        std::vector<uint32_t> strm(d->nwords);
+        if (d->nwords) HIP_TRY(c, hipMemcpy(strm.data(), d->cols.stream, d->nwords * 4, hipMemcpyDeviceToHost));
+        std::vector<size_t> idx(n);
+        for (size_t i = 0; i < n; i++) idx[i] = i;
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
+            return tid[x] != tid[y] ? tid[x] < tid[y] : pos[x] < pos[y];
+        });
+        std::vector<int32_t> p2(n), e2(n);
+        std::vector<uint32_t> n2(n), s2;
+        std::vector<uint64_t> o2(n + 1);
+        s2.reserve(d->nwords);
+        std::fill(toff.begin(), toff.end(), 0);
+        for (size_t k = 0; k < n; k++) {
+            const size_t i = idx[k];
+            p2[k] = pos[i]; e2[k] = endpos[i]; n2[k] = nc[i];
+            o2[k] = s2.size();
+            s2.insert(s2.end(), strm.begin() + (ptrdiff_t)soff[i], strm.begin() + (ptrdiff_t)soff[i + 1]);
+            toff[(size_t)tid[i] + 1]++;
+        }
+        o2[n] = s2.size();
+        for (int32_t t = 0; t < nt; t++) toff[(size_t)t + 1] += toff[(size_t)t];
+        s = load_core(c, nt, toff.data(), p2.data(), e2.data(), n2.data(), o2.data(), s2.data(), nullptr,
+                      d->stats.cigar_ops, pre);
+    } else {
+        // the stream stays where the decode wrote it (its spare words zeroed): the context adopts it
+        HIP_TRY(c, hipMemset(d->cols.stream + d->nwords, 0, STREAM_PAD * 4));
+        s = load_core(c, nt, toff.data(), pos.data(), endpos.data(), nc.data(), soff.data(), nullptr, d->cols.stream,
+                      d->stats.cigar_ops, pre);
+        if (c->d_cigar == d->cols.stream) {
+            d->cols.stream = nullptr;
+            d->word_cap = 0;
+        }
+    }
+    c->load_stats.total_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return s;
+}
+
+void svt_bam_dec_close(svt_bam_dec *d) {
+    if (!d) return;
+    {
+        DevGuard dg(d->c->device);
+        if (d->st) (void)hipStreamSynchronize(d->st);
+        hfree(d->d_comp); hfree(d->d_blk); hfree(d->d_buf[0]); hfree(d->d_buf[1]);
+        hfree(d->d_ch); hfree(d->d_base); hfree(d->d_rec); hfree(d->d_pre); hfree(d->d_chk); hfree(d->d_tmp);
+        hfree(d->cols.tid); hfree(d->cols.pos); hfree(d->cols.endpos); hfree(d->cols.nc); hfree(d->cols.soff);
+        hfree(d->cols.stream);
+        if (d->st) (void)hipStreamDestroy(d->st);
+    }
+    delete d;
 }
 
 void svt_close(svt_ctx *c) {

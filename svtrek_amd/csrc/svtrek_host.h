@@ -51,6 +51,24 @@ typedef struct svth_inflater {
  * inf == NULL: host threads inflate. */
 svth_bam *svth_bam_read_ex(const char *path, int threads, int32_t tid0, int64_t beg0, int32_t tid1, int64_t end1,
                            const svth_inflater *inf, char *err, size_t errcap);
+/* A BAM decoded on the device: the file read in batches of whole BGZF blocks (`threads`
+ * parallel preads; buffers from sink->alloc when given, e.g. pinned memory) and handed to
+ * sink->feed compressed -- the next batch read by a helper thread meanwhile.  The header is
+ * inflated and read on the host: sink->begin gets its reference count first, and the first
+ * feed's `skip` is its length in the inflated stream (the CLI's sink is svt_bam_dec_*).
+ * stage4 (optional): batch reads, feed calls, waits for the next batch, the whole read (s).
+ * Returns 0, or 1 with a message in err. */
+typedef struct svth_dev_sink {
+    int (*begin)(void *user, int32_t n_targets, char *err, size_t errcap);
+    int (*feed)(void *user, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks, size_t n,
+                uint64_t skip, char *err, size_t errcap);
+    void *(*alloc)(void *user, size_t bytes);
+    void (*release)(void *user, void *p);
+    void *user;
+    size_t batch_bytes;   /* compressed bytes per batch (0: 1 GiB) */
+} svth_dev_sink;
+int svth_bam_read_device(const char *path, int threads, const svth_dev_sink *sink, int32_t *n_targets, double *stage4,
+                         char *err, size_t errcap);
 void      svth_bam_free(svth_bam *b);
 /* View valid until svth_bam_free. */
 void      svth_bam_view(const svth_bam *b, svt_pileup_view *out);

@@ -275,6 +275,44 @@ int device_inflate(void *user, const uint8_t *comp, size_t cb, const svt_bgzf_bl
     return 0;
 }
 
+// The ingest's device sink (svt_bam_dec_*): BAM batches go to the first device compressed and
+// are inflated and decoded there into the pileup (one device; --gpus N > 1 parses on the host).
+struct DeviceDecode {
+    std::shared_future<void> ready;
+    svt_ctx **ctx;
+    const int *open_rc;
+    svt_bam_dec *dec = nullptr;
+    bool pinned = true;   // batch buffers in pinned host memory (SVTREK_DEC_PINNED=0: pageable)
+};
+int dd_begin(void *user, int32_t n_targets, char *err, size_t ecap) {
+    DeviceDecode *d = (DeviceDecode *)user;
+    d->ready.wait();
+    if (*d->open_rc || !*d->ctx) { snprintf(err, ecap, "BAM decode: svt_open failed (HIP device?)"); return 1; }
+    if (svt_bam_dec_open(*d->ctx, n_targets, &d->dec) != SVT_OK) {
+        snprintf(err, ecap, "BAM decode: %s", svt_last_error(*d->ctx));
+        return 1;
+    }
+    return 0;
+}
+int dd_feed(void *user, const uint8_t *comp, size_t cb, const svt_bgzf_block *blocks, size_t n, uint64_t skip, char *err,
+            size_t ecap) {
+    DeviceDecode *d = (DeviceDecode *)user;
+    if (svt_bam_dec_feed(d->dec, comp, cb, blocks, n, skip) != SVT_OK) {
+        snprintf(err, ecap, "BAM decode on the device: %s", svt_last_error(*d->ctx));
+        return 1;
+    }
+    return 0;
+}
+void *dd_alloc(void *user, size_t bytes) {
+    DeviceDecode *d = (DeviceDecode *)user;
+    d->ready.wait();
+    return !d->pinned || *d->open_rc || !*d->ctx ? nullptr : svt_host_alloc(*d->ctx, bytes);   // nullptr: malloc
+}
+void dd_release(void *user, void *p) {
+    DeviceDecode *d = (DeviceDecode *)user;
+    svt_host_free(*d->ctx, p);
+}
+
 int audit(int argc, char **argv) {
     Args a = parse_audt(argc, argv);
     const double t0 = now_s();
@@ -313,21 +351,41 @@ int audit(int argc, char **argv) {
     size_t batch_mb = 1024;
     if (const char *x = getenv("SVTREK_INFLATE_BATCH_MB")) batch_mb = std::max<size_t>(1, strtoull(x, nullptr, 10));
     const svth_inflater dev_inf{device_inflate, device_host_alloc, device_host_free, &dinf, batch_mb << 20};
-    svth_bam *bam = svth_bam_read_ex(a.bam, a.threads, -1, 0, -1, 0, a.gpu_inflate ? &dev_inf : nullptr, err, sizeof err);
+    // one GPU: the records are decoded on the device too (svt_bam_dec_*; SVTREK_HOSTPARSE=1: the
+    // device inflates, the host parses, as for --gpus N > 1)
+    const char *hp = getenv("SVTREK_HOSTPARSE");
+    const bool dev_decode = a.gpu_inflate && G == 1 && !(hp && atoi(hp) == 1);
+    DeviceDecode ddec{dinf.ready, &ctxs[0], &open_rc[0]};
+    if (const char *x = getenv("SVTREK_DEC_PINNED")) ddec.pinned = atoi(x) != 0;
+    const svth_dev_sink dsink{dd_begin, dd_feed, dd_alloc, dd_release, &ddec, batch_mb << 20};
+    svth_bam *bam = nullptr;
+    double dstage[4] = {0, 0, 0, 0};
+    int dec_rc = 0;
+    if (dev_decode) dec_rc = svth_bam_read_device(a.bam, a.threads, &dsink, nullptr, dstage, err, sizeof err);
+    else bam = svth_bam_read_ex(a.bam, a.threads, -1, 0, -1, 0, a.gpu_inflate ? &dev_inf : nullptr, err, sizeof err);
     const double t_ingest = now_s();
     vt.join();
     ot.join();
-    if (!bam) { fprintf(stderr, "[ERROR] %s\n", err); svth_vcf_free(pv); close_all(); return 1; }
-    if (!vcf_ok) {
-        fprintf(stderr, "[ERROR]: File couldn't be opened %s\n", a.vcf);
-        svth_bam_free(bam);
+    if (dev_decode ? dec_rc != 0 : !bam) {
+        fprintf(stderr, "[ERROR] %s\n", err);
+        svt_bam_dec_close(ddec.dec);
+        svth_vcf_free(pv);
         close_all();
         return 1;
     }
-    double stage[6];
-    svth_bam_stage_seconds(bam, stage);
-    svt_pileup_view view;
-    svth_bam_view(bam, &view);
+    if (!vcf_ok) {
+        fprintf(stderr, "[ERROR]: File couldn't be opened %s\n", a.vcf);
+        svth_bam_free(bam);
+        svt_bam_dec_close(ddec.dec);
+        close_all();
+        return 1;
+    }
+    double stage[6] = {0, 0, 0, 0, 0, 0};
+    svt_pileup_view view{};
+    if (bam) {
+        svth_bam_stage_seconds(bam, stage);
+        svth_bam_view(bam, &view);
+    }
     size_t mlen = 0;
     const char *msgs = svth_vcf_messages(pv, &mlen);
     if (mlen) fwrite(msgs, 1, mlen, stderr);
@@ -364,6 +422,10 @@ int audit(int argc, char **argv) {
             in = sh.loci.data();
             out = sh.res.data();
             n = sh.loci.size();
+        } else if (ddec.dec) {   // decoded on this device: its pileup, in place
+            s = svt_bam_dec_load(ddec.dec);
+            svt_bam_dec_close(ddec.dec);
+            ddec.dec = nullptr;
         } else {
             s = svt_load_pileup(ctx, &view);
         }
@@ -397,13 +459,17 @@ int audit(int argc, char **argv) {
     svth_free(out);
     printf("[INFO] Ended processing variation file\n");
     if (a.verbose)   // --verbose is parsed but unused by the reference; here: stage timings on stderr
-        fprintf(stderr, "[svtrek_amd] ingest %.3fs (inflate %s%s)  vcf-read+parse %.3fs (beside the ingest)  "
+        fprintf(stderr, "[svtrek_amd] ingest %.3fs (%s%s)  vcf-read+parse %.3fs (beside the ingest)  "
                         "load+refine %.3fs (load %.3fs)  print %.3fs  records %zu\n",
-                t_ingest - t0, a.gpu_inflate ? "gpu, kernels " : "cpu",
-                a.gpu_inflate ? (std::to_string(dinf.ms / 1e3).substr(0, 5) + "s; batch read " +
-                                 std::to_string(stage[0]).substr(0, 5) + "s alloc " + std::to_string(stage[2]).substr(0, 5) +
-                                 "s inflate calls " + std::to_string(stage[3]).substr(0, 5) + "s parser waits " +
-                                 std::to_string(stage[4]).substr(0, 5) + "s").c_str() : "",
+                t_ingest - t0,
+                dev_decode ? "gpu inflate + record decode" : a.gpu_inflate ? "gpu inflate, host parse, kernels " : "cpu",
+                dev_decode ? ("; batch reads " + std::to_string(dstage[0]).substr(0, 5) + "s device feeds " +
+                              std::to_string(dstage[1]).substr(0, 5) + "s waits " + std::to_string(dstage[2]).substr(0, 5) +
+                              "s").c_str()
+                : a.gpu_inflate ? (std::to_string(dinf.ms / 1e3).substr(0, 5) + "s; batch read " +
+                                   std::to_string(stage[0]).substr(0, 5) + "s alloc " + std::to_string(stage[2]).substr(0, 5) +
+                                   "s inflate calls " + std::to_string(stage[3]).substr(0, 5) + "s parser waits " +
+                                   std::to_string(stage[4]).substr(0, 5) + "s").c_str() : "",
                 t_parse_end - t0, t_refine - t_parse, *std::max_element(load_s.begin(), load_s.end()),
                 now_s() - t_refine, loci.size());
     return 0;

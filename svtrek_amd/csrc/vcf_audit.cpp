@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -67,10 +68,58 @@ struct svth_vcf {
 
 extern "C" {
 
+// One logical VCF line of process_vcf's reader (audit.c:299-327) -> o.
+static void vcf_take(char *line, svth_vcf &o, char *perr, size_t cap) {
+    svt_locus l;
+    const int act = svth_parse_line(line, &l, perr, cap);
+    if (act == 2) o.msgs += perr;
+    if (act != 1) return;
+    if (svth_is_unknown_type(&l)) o.msgs += "[ERROR] Unkown type.\n";
+    o.loci.push_back(l);
+}
+
+// The reader loop of audit.c:294-327 exactly, sequentially: fgets into a buffer of current_size
+// bytes (1 MiB, doubled whenever a line fills it, never shrunk), strlen (a line ends at its
+// first NUL; the rest of what that fgets read is dropped), a final line without '\n' that exactly
+// fills the buffer skipped (the next fgets returns NULL, :317), lines shorter than 2 chars and
+// '#' lines skipped.  Used when the file has a line of 1 MiB or more (the buffer's history
+// matters then); svth_vcf_parse's threaded loop is the same for every shorter line.
+static void vcf_parse_exact(const char *text, size_t len, svth_vcf &o) {
+    size_t cur = 1u << 20, pos = 0;
+    std::string buf(cur, '\0');
+    char perr[1024];
+    // fgets(buf + at, cap): up to cap - 1 chars through the first '\n'; false (NULL) at the end
+    auto fgets_at = [&](size_t at, size_t cap) {
+        if (pos >= len) return false;
+        const size_t room = std::min(cap - 1, len - pos);
+        const void *nl = memchr(text + pos, '\n', room);
+        const size_t k = nl ? (size_t)((const char *)nl - (text + pos)) + 1 : room;
+        memcpy(&buf[at], text + pos, k);
+        buf[at + k] = '\0';
+        pos += k;
+        return true;
+    };
+    while (fgets_at(0, cur)) {
+        size_t n = strlen(buf.c_str());
+        bool skip = false;
+        while (n == cur - 1 && buf[n - 1] != '\n') {   // audit.c:304-319
+            cur *= 2;
+            buf.resize(cur);
+            if (!fgets_at(n, cur - n)) { skip = true; break; }
+            n = strlen(buf.c_str());
+        }
+        if (skip || n < 2 || buf[0] == '#') continue;   // :321-322
+        if (buf[n - 1] == '\n') n--;                     // :324-327
+        std::string line(buf.data(), n);
+        vcf_take(&line[0], o, perr, sizeof perr);
+    }
+}
+
 svth_vcf *svth_vcf_parse(const char *text, size_t len, int threads) {
     const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), len / (1u << 20) + 1));
     const std::vector<size_t> cut = line_cuts(text, len, T);
     std::vector<svth_vcf> part((size_t)T);
+    std::atomic<bool> long_line{false};
     run_parts(T, [&](int t) {
         svth_vcf &o = part[(size_t)t];
         std::string line;
@@ -80,17 +129,21 @@ svth_vcf *svth_vcf_parse(const char *text, size_t len, int threads) {
             const size_t n = (nl ? (size_t)((const char *)nl - text) + 1 : e) - i;
             const char *ln = text + i;
             i += n;
-            if (n < 2 || ln[0] == '#') continue;                 // audit.c:324-325
-            line.assign(ln, ln[n - 1] == '\n' ? n - 1 : n);     // :327-330
-            svt_locus l;
-            const int act = svth_parse_line(&line[0], &l, perr, sizeof perr);
-            if (act == 2) o.msgs += perr;
-            if (act != 1) continue;
-            if (svth_is_unknown_type(&l)) o.msgs += "[ERROR] Unkown type.\n";
-            o.loci.push_back(l);
+            // a physical line of 1 MiB - 1 chars or more: the reader's buffer history decides
+            // (vcf_parse_exact); shorter ones are one fgets each
+            if (n >= (1u << 20) - 1) { long_line = true; return; }
+            const void *z = memchr(ln, '\0', n);               // strlen: the line ends at a NUL
+            const size_t m = z ? (size_t)((const char *)z - ln) : n;
+            if (m < 2 || ln[0] == '#') continue;                     // audit.c:321-322
+            line.assign(ln, ln[m - 1] == '\n' ? m - 1 : m);         // :324-327
+            vcf_take(&line[0], o, perr, sizeof perr);
         }
     });
     svth_vcf *v = new svth_vcf();
+    if (long_line) {
+        vcf_parse_exact(text, len, *v);
+        return v;
+    }
     size_t n = 0;
     for (auto &p : part) n += p.loci.size();
     v->loci.reserve(n);

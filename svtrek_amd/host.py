@@ -28,6 +28,8 @@ def load_host() -> C.CDLL:
         L.svth_bam_read_ex.argtypes = [C.c_char_p, C.c_int, C.c_int32, C.c_int64, C.c_int32, C.c_int64, P,
                                        C.c_char_p, C.c_size_t]
         L.svth_bam_read_ex.restype = P
+        L.svth_bam_read_device.argtypes = [C.c_char_p, C.c_int, P, P, P, C.c_char_p, C.c_size_t]
+        L.svth_bam_read_device.restype = C.c_int
         L.svth_vcf_parse.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
         L.svth_vcf_parse.restype = P
         L.svth_vcf_count.argtypes = [P]
@@ -75,6 +77,60 @@ RELEASE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p)
 class SvthInflater(C.Structure):
     _fields_ = [("inflate", C.c_void_p), ("alloc", C.c_void_p), ("release", C.c_void_p), ("user", C.c_void_p),
                 ("batch_bytes", C.c_size_t)]
+
+
+BEGIN_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t)
+FEED_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_uint64, C.c_void_p,
+                      C.c_size_t)
+
+
+class SvthDevSink(C.Structure):
+    _fields_ = [("begin", C.c_void_p), ("feed", C.c_void_p), ("alloc", C.c_void_p), ("release", C.c_void_p),
+                ("user", C.c_void_p), ("batch_bytes", C.c_size_t)]
+
+
+def load_bam_device(engine, path: str, threads: int = 4, batch_bytes: int = 0, pinned: bool = True) -> dict:
+    """The BAM decoded on the engine's device (svth_bam_read_device feeding svt_bam_dec_*: BGZF
+    inflate + record decode there) and loaded as the engine's pileup; returns the decoder's
+    stats and the reader's stage times.  The same as engine.load_pileup(read_bam(path)[0])."""
+    from ._lib import SvtBamDecStats
+    L = load_host()
+    lib, ctx = engine.lib, engine._h
+    dec = C.c_void_p()
+    err = C.create_string_buffer(512)
+
+    def put(e, ecap, m: bytes) -> None:
+        m = m[:max(int(ecap) - 1, 0)]
+        C.memmove(e, m + b"\0", len(m) + 1)
+
+    def begin(_u, nt, e, ecap):
+        rc = lib.svt_bam_dec_open(ctx, nt, C.byref(dec))
+        if rc:
+            put(e, ecap, lib.svt_last_error(ctx))
+        return 1 if rc else 0
+
+    def feed(_u, comp, cb, blocks, n, skip, e, ecap):
+        rc = lib.svt_bam_dec_feed(dec, comp, cb, blocks, n, skip)
+        if rc:
+            put(e, ecap, lib.svt_last_error(ctx))
+        return 1 if rc else 0
+    fb, ff = BEGIN_FN(begin), FEED_FN(feed)
+    fa = ALLOC_FN(lambda _u, n: lib.svt_host_alloc(ctx, n))
+    fr = RELEASE_FN(lambda _u, p: lib.svt_host_free(ctx, p))
+    sink = SvthDevSink(C.cast(fb, C.c_void_p), C.cast(ff, C.c_void_p), C.cast(fa, C.c_void_p) if pinned else None,
+                       C.cast(fr, C.c_void_p) if pinned else None, None, batch_bytes)
+    st4 = (C.c_double * 4)()
+    try:
+        if L.svth_bam_read_device(path.encode(), threads, C.byref(sink), None, st4, err, 512) != 0:
+            raise OSError(err.value.decode())
+        engine._check(lib.svt_bam_dec_load(dec))
+        st = SvtBamDecStats()
+        engine._check(lib.svt_bam_dec_stats_get(dec, C.byref(st)))
+    finally:
+        lib.svt_bam_dec_close(dec)
+    out = {k: getattr(st, k) for k, _ in SvtBamDecStats._fields_}
+    out["stage_s"] = dict(zip(("read", "feed", "wait", "total"), (round(x, 4) for x in st4)))
+    return out
 
 
 def read_bam(path: str, threads: int = 4, region: tuple[int, int, int, int] | None = None,

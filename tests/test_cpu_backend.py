@@ -57,13 +57,17 @@ def test_cpu_backend_errors():
             e.refine(make_loci([(2, 1, 1000, 5000)]))   # before load_pileup: SVT_ESTATE
 
 
-@pytest.mark.parametrize("inflate", ["cpu", "gpu"])
+@pytest.mark.parametrize("inflate", ["cpu", "gpu", "gpu-hostparse"])
 def test_cli_on_cpu_backend(tmp_path, inflate, monkeypatch):
     """The drop-in CLI's whole flow (BAM ingest, parallel A1 parse beside it, batched refine,
     batch A11 print) linked against the CPU backend: stdout bytes equal the oracle's.
-    --inflate gpu runs the ingest's batch pipeline (here through the CPU backend's
-    svt_bgzf_inflate, zlib) in 1 MiB batches."""
+    --inflate gpu runs the ingest's device pipeline in 1 MiB batches: the batches handed to
+    svt_bam_dec_* (here the CPU backend's decoder), or -- gpu-hostparse, SVTREK_HOSTPARSE=1 --
+    inflated by svt_bgzf_inflate and parsed on the host."""
     monkeypatch.setenv("SVTREK_INFLATE_BATCH_MB", "1")
+    if inflate == "gpu-hostparse":
+        monkeypatch.setenv("SVTREK_HOSTPARSE", "1")
+        inflate = "gpu"
     r = sim.generate(sim.SimConfig(seed=41, n_targets=2, n_loci=150, del_frac=0.5, coverage=10), keep_handle=True)
     bam = str(tmp_path / "c.bam")
     sim.write_bam(r, bam, with_seq=True, level=1)

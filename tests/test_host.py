@@ -300,3 +300,80 @@ def test_bam_read_with_inflate_callback(tmp_path, region):
     assert wi == gi
     for k in ("tid_off", "pos", "endpos", "cig_off", "cigar", "clip"):
         assert np.array_equal(getattr(want, k), getattr(got, k)), k
+
+
+def _reference_reader(data: bytes) -> list[bytes]:
+    """The reader loop of audit.c:294-327, restated over bytes: fgets into a buffer of
+    current_size bytes (1 MiB, doubled whenever a line fills it, never shrunk), strlen, the
+    skip of a final line that exactly fills the buffer (fgets returns NULL, :317), of lines
+    shorter than 2 chars and of '#' lines; the trailing '\\n' stripped."""
+    cur, pos, n, out = 1 << 20, 0, len(data), []
+
+    def fgets(cap):
+        nonlocal pos
+        if pos >= n:
+            return None
+        room = min(cap - 1, n - pos)
+        j = data.find(b"\n", pos, pos + room)
+        k = j - pos + 1 if j >= 0 else room
+        s = data[pos:pos + k]
+        pos += k
+        return s
+
+    def strlen(b):
+        z = b.find(b"\0")
+        return len(b) if z < 0 else z
+
+    while (buf := fgets(cur)) is not None:
+        L, skip = strlen(buf), False
+        while L == cur - 1 and buf[L - 1:L] != b"\n":
+            cur *= 2
+            t = fgets(cur - L)
+            if t is None:
+                skip = True
+                break
+            buf = buf[:L] + t
+            L = strlen(buf)
+        if skip or L < 2 or buf[:1] == b"#":
+            continue
+        line = buf[:L]
+        out.append(line[:-1] if line.endswith(b"\n") else line)
+    return out
+
+
+def _padded_record(pos: int, total: int, nl: bool) -> bytes:
+    """A DEL record whose line is exactly `total` bytes (the trailing '\\n' included when nl)."""
+    head = f"1\t{pos}\t.\tN\t<DEL>\t.\tPASS\tSVTYPE=DEL;END={pos + 900};PAD=".encode()
+    return head + b"x" * (total - len(head) - (1 if nl else 0)) + (b"\n" if nl else b"")
+
+
+@pytest.mark.parametrize("case", ["final_fills_1m", "final_short_by_one", "grown_buffer", "final_fills_2m",
+                                  "long_mid", "nul"])
+def test_vcf_reader_long_lines_and_nul(case):
+    """svth_vcf_parse (threaded; the exact sequential reader once a line reaches 1 MiB) and the
+    oracle's orc_audit_text against the reference's reader loop (audit.c:294-327): a final line
+    without '\\n' that exactly fills the 1 MiB buffer is dropped; after a longer line has grown the
+    buffer to 2 MiB the same line is kept and a 2 MiB - 1 one dropped; a NUL ends a line."""
+    body = b"".join(_padded_record(10000 + 5000 * k, 90, True) for k in range(20))
+    M = 1 << 20
+    tail = {"final_fills_1m": _padded_record(900000, M - 1, False),
+            "final_short_by_one": _padded_record(900000, M - 2, False),
+            "grown_buffer": _padded_record(800000, M + 300, True) + _padded_record(900000, M - 1, False),
+            "final_fills_2m": _padded_record(800000, M + 300, True) + _padded_record(900000, 2 * M - 1, False),
+            "long_mid": _padded_record(800000, 3 * M + 7, True) + body,
+            "nul": b"1\t700000\t.\tN\t<DEL>\t.\tPASS\tSVTYPE=DEL;END=700900\x00;junk\n" + b"1\t7\0\n"}[case]
+    data = body + tail
+    want = _reference_reader(data)
+    recs = [host.parse_line(w.decode("latin-1")) for w in want]
+    want_loci = [r[1] for r in recs if r[0] == 1]
+    for threads in (1, 4):
+        loci, _ = host.parse_vcf_text(data, threads=threads)
+        assert [tuple(int(x) for x in r) for r in loci] == want_loci, (case, threads)
+    # the oracle's reader: one printed line per parsed record (an empty pileup: NA results)
+    from svtrek_amd.pileup import from_reads
+    printed = O.audit_text(data.decode("latin-1"), from_reads(1, [])).splitlines()[1:-1]
+    assert len(printed) == len(want_loci), case
+    if case == "final_fills_1m":
+        assert len(want_loci) == 20   # the final line is dropped
+    if case in ("final_short_by_one", "grown_buffer"):
+        assert len(want_loci) == 21 + (case == "grown_buffer")
