@@ -1720,7 +1720,7 @@ struct svt_ctx {
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
     uint64_t ix_ranges = 65536;   // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
-    int lane_w = 0;               // SVTREK_LANE_W=8|32 forces the lane kernel's windows per wave (A/B)
+    int lane_w = 0;               // SVTREK_LANE_W=32 forces the lane kernel at every batch size (tests)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
     uint32_t lane_par = 0;        // which of the two redo counters the next lane launch uses
@@ -1934,12 +1934,8 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
         a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + c->lane_par;
         a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->lane_par ^ 1u);
         c->lane_par ^= 1u;
-        if (c->lane_w == 8)
-            hipLaunchKernelGGL(refine_lane_kernel<8>, dim3((unsigned)((2 * n + WPB * 8 - 1) / (WPB * 8))), block, 0,
-                               st, a);
-        else
-            hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
-                               st, a);
+        hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
+                           st, a);
         hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
     } else {
         hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
@@ -2129,7 +2125,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *x = getenv("SVTREK_IX")) c->ix_mode = strcmp(x, "lane") == 0 ? 1 : strcmp(x, "stream") == 0 ? 2 : 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
-    if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 8 ? 8 : atoi(lw) == 32 ? 32 : 0;
+    if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;

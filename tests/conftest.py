@@ -29,11 +29,11 @@ def engine_factory():
     engines = []
 
     # gather variant -> (SVTREK_GATHER, SVTREK_LANE_W)
-    variants = {"span": ("span", "32"), "lane8": ("span", "8"), "auto": ("span", None), "span1": ("span1", None)}
+    variants = {"span": ("span", "32"), "auto": ("span", None), "span1": ("span1", None)}
 
     def make(params=None, gather="span", env=None):
         """gather: "span" (span events through refine_lane_kernel<32> at every batch size -- the
-        product picks it from 64K windows up), "lane8" (refine_lane_kernel<8>), "span1" (one wave per
+        product picks it from 64K windows up), "span1" (one wave per
         window, refine_span_kernel: the product's pick for smaller batches) or "auto" (the product's
         size-based pick).  env: extra engine switches read at svt_open (e.g. SVTREK_IX_EXACT=1)."""
         g, lw = variants.get(gather, (gather, None))

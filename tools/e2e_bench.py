@@ -29,8 +29,10 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--level", type=int, default=1, help="BGZF deflate level for the written BAM")
     ap.add_argument("--dir", default=None)
-    ap.add_argument("--inflate", default="gpu,cpu", help="BGZF inflate modes to time (CLI --inflate), comma-separated; "
-                    "gpu:MB sets the device batch (SVTREK_INFLATE_BATCH_MB)")
+    ap.add_argument("--inflate", default="gpu,gpuhost,cpu",
+                    help="ingest modes to time, comma-separated: gpu (BGZF inflate + record decode on the device, "
+                         "svt_bam_dec_*), gpuhost (device inflate, host record parse: SVTREK_HOSTPARSE=1), cpu (host "
+                         "threads); gpu:MB / gpuhost:MB set the batch (SVTREK_INFLATE_BATCH_MB)")
     ap.add_argument("--region-sample", type=int, default=0, metavar="K",
                     help="the CPU baseline's sample instead of the whole workload: the first K loci of contig 1 "
                          "(genomic order) and the BAM of their region, with SEQ/QUAL -- the same bytes bench.py's "
@@ -65,8 +67,12 @@ def main() -> int:
             env = dict(os.environ)
             if ":" in mode:
                 env["SVTREK_INFLATE_BATCH_MB"] = mode.split(":")[1]
+            base = mode.split(":")[0]
+            if base == "gpuhost":
+                env["SVTREK_HOSTPARSE"] = "1"
             p = subprocess.run([cli, "audt", "-b", bam, "-v", vcf, "-t", str(a.t), "--verbose", "--inflate",
-                                mode.split(":")[0]], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=1800, env=env)
+                                "gpu" if base == "gpuhost" else base], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                               timeout=1800, env=env)
             times.append(time.perf_counter() - t)
             if p.returncode != 0:
                 print(p.stderr.decode()[-2000:], file=sys.stderr)
