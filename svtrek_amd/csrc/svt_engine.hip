@@ -39,7 +39,6 @@
 #include <vector>
 
 #include "../../include/svtrek_gpu.h"
-#include "svt_inflate.h"
 #include "svt_bamrec.h"
 
 #define SVT_VERSION "svtrek_amd 0.17.0 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
@@ -1690,27 +1689,7 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 #include "svt_poa.inc"
 #include "svt_bam.inc"
 
-// ------------------------------------------------------------------ BGZF inflate
-// One lane per BGZF block (svt_inflate.h): a BAM's blocks are independent DEFLATE streams of
-// <= 64 KiB output, so a batch of them fills the chip with no cross-lane work.  The primary
-// Huffman tables of the wave's 64 blocks are interleaved in LDS (entry i of lane l at
-// i * 64 + l: conflict-free for any mix of indices), the slow-path arrays and code lengths in
-// a per-lane global scratch slot.  A persistent grid: lane g takes blocks g, g + G, ...
-constexpr int INF_GRID = 4096;   // workgroups (one wave each) at most: <= 262144 scratch slots
-__global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *comp, const svt_bgzf_block *blk, uint32_t n,
-                                                     uint8_t *out, InfSlow *scratch, uint32_t *err) {
-    __shared__ uint16_t tabs[IF_FAST * WAVE];
-    const uint32_t ln = threadIdx.x;
-    const uint32_t g = blockIdx.x * WAVE + ln;
-    const InfFast F(tabs + ln, WAVE);
-    for (uint32_t b = g; b < n; b += gridDim.x * WAVE) {
-        const svt_bgzf_block k = blk[b];
-        const uint64_t a = k.coff & ~15ull;
-        const int rc = inf_block(reinterpret_cast<const InfV4 *>(comp + a), (uint32_t)(k.coff - a), k.clen,
-                                 out + k.uoff, k.ulen, F, scratch[g]);
-        if (rc != INF_OK) atomicMin(err, b);
-    }
-}
+#include "svt_inflate.inc"
 
 }  // namespace
 
@@ -1778,7 +1757,6 @@ struct svt_ctx {
     // BGZF inflate (svt_bgzf_inflate): device buffers grown on demand, never shrunk
     uint8_t *d_infc = nullptr, *d_info = nullptr;
     svt_bgzf_block *d_infb = nullptr;
-    InfSlow *d_infs = nullptr;
     uint32_t *d_inferr = nullptr;
     size_t infc_cap = 0, info_cap = 0, infb_cap = 0;
     double inf_ms = 0;                // device time of the last svt_bgzf_inflate's kernel
@@ -2803,15 +2781,13 @@ svt_status svt_bgzf_inflate_device(svt_ctx *c, const uint8_t *d_comp, const svt_
     if (n > 0xfffffffeull) return fail(c, SVT_EINVAL, "%s", "more than 2^32 - 2 blocks in one call");
     DEV_GUARD(c);
     const hipStream_t st = (hipStream_t)stream;
-    const unsigned grid = (unsigned)std::min<size_t>((n + WAVE - 1) / WAVE, (size_t)INF_GRID);
-    if (!c->d_infs) HIP_TRY(c, hipMalloc(&c->d_infs, (size_t)INF_GRID * WAVE * sizeof(InfSlow)));
+    const unsigned grid = (unsigned)std::min<size_t>(n, (size_t)INF_GRID);
     if (!c->d_inferr) HIP_TRY(c, hipMalloc(&c->d_inferr, sizeof(uint32_t)));
     // the scratch slots and the error word are per context: calls on different streams run in
     // submission order (like every other launch of the context)
     if (svt_status s = order_on(c, st)) return s;
     HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, st, d_comp, d_blocks, (uint32_t)n, d_out, c->d_infs,
-                       c->d_inferr);
+    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, st, d_comp, d_blocks, (uint32_t)n, d_out, c->d_inferr);
     HIP_TRY(c, hipGetLastError());
     return SVT_OK;
 }
@@ -2954,10 +2930,6 @@ svt_status svt_bam_dec_open(svt_ctx *c, int32_t n_targets, svt_bam_dec **out) {
         svt_bam_dec_close(d);
         return fail(c, SVT_EDEVICE, "%s", "BAM decode: stream / buffers");
     }
-    if (!c->d_infs && hipMalloc(&c->d_infs, (size_t)INF_GRID * WAVE * sizeof(InfSlow)) != hipSuccess) {
-        svt_bam_dec_close(d);
-        return fail(c, SVT_ENOMEM, "%s", "inflate scratch");
-    }
     if (!c->d_inferr && hipMalloc(&c->d_inferr, sizeof(uint32_t)) != hipSuccess) {
         svt_bam_dec_close(d);
         return fail(c, SVT_ENOMEM, "%s", "inflate scratch");
@@ -2994,9 +2966,9 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
         HIP_TRY(c, hipMemcpyAsync(d->d_comp, comp, comp_bytes, hipMemcpyHostToDevice, d->st));
         HIP_TRY(c, hipMemcpyAsync(d->d_blk, blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->st));
         HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), d->st));
-        const unsigned grid = (unsigned)std::min<size_t>((n + WAVE - 1) / WAVE, (size_t)INF_GRID);
+        const unsigned grid = (unsigned)std::min<size_t>(n, (size_t)INF_GRID);
         hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, d->st, d->d_comp, d->d_blk, (uint32_t)n, buf + T,
-                           c->d_infs, c->d_inferr);
+                           c->d_inferr);
         HIP_TRY(c, hipGetLastError());
     }
     const uint64_t span = N - r0;
@@ -3200,7 +3172,7 @@ void svt_close(svt_ctx *c) {
     DevGuard dg(c->device);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     free_pileup(c);
-    hfree(c->d_infc); hfree(c->d_info); hfree(c->d_infb); hfree(c->d_infs); hfree(c->d_inferr);
+    hfree(c->d_infc); hfree(c->d_info); hfree(c->d_infb); hfree(c->d_inferr);
     hfree(c->d_loci); hfree(c->d_out); hfree(c->d_pool); hfree(c->d_ctl); hfree(c->d_redo); hfree(c->poa_small.d); hfree(c->poa_big.d);
     delete c;
 }

@@ -1,8 +1,9 @@
-"""svt_bgzf_inflate on the device: BGZF blocks inflated one lane per block,
-byte-identical to zlib -- a BAM with SEQ/QUAL written by the simulator's BGZF writer, and raw
-DEFLATE streams of every block type (stored / fixed / dynamic, zlib's strategies), mixed in
-one batch at arbitrary byte alignments; a corrupt block is reported by index; the CPU backend
-(zlib) behind the same ABI agrees."""
+"""svt_bgzf_inflate on the device: BGZF blocks inflated one wave per block
+(svt_inflate.inc), byte-identical to zlib -- a BAM with SEQ/QUAL written by the simulator's BGZF
+writer, and raw DEFLATE streams of every block type (stored / fixed / dynamic), zlib level and
+strategy, data kind (tests/deflate_streams.py) and byte alignment of input and output, mixed in
+one batch; corrupt streams (truncated, wrong ISIZE, reserved block type, codes zlib rejects) are
+reported by block index; the CPU backend (zlib) behind the same ABI agrees."""
 import ctypes as C
 import os
 import random
@@ -11,6 +12,7 @@ import zlib
 import numpy as np
 import pytest
 
+import deflate_streams as D
 from svtrek_amd import Engine, Params, sim
 from svtrek_amd._lib import BGZF_BLOCK_DTYPE, bind_abi
 from svtrek_amd.bgzf import block_table
@@ -34,6 +36,51 @@ def test_inflate_sim_bam(engine_factory, tmp_path):
     got = eng.bgzf_inflate(comp, blocks)
     assert got.tobytes() == _zlib_all(comp, blocks)
     assert len(blocks) > 50 and eng.last_inflate_ms() > 0
+
+
+def _batch(streams, rng, out_skew=False):
+    """(comp bytes, block table) for [(compressed, plain)], each at a random input alignment
+    (and, with out_skew, a random output gap)."""
+    comp, rows, u = bytearray(), [], 0
+    for z, d in streams:
+        comp += bytes(rng.randint(0, 7))
+        rows.append((len(comp), u, len(z), len(d)))
+        comp += z
+        u += len(d) + (rng.randint(0, 5) if out_skew else 0)
+    return bytes(comp), np.array(rows, dtype=BGZF_BLOCK_DTYPE)
+
+
+def test_inflate_every_kind_level_strategy(engine_factory):
+    """Every data kind x zlib level x strategy, at random input / output alignments."""
+    rng = random.Random(11)
+    streams = []
+    for kind in D.KINDS:
+        d = D.data(kind, rng)
+        for level in (0, 1, 6, 9):
+            for strat in D.STRATEGIES:
+                streams.append((D.deflate(d, level, strat), d))
+    rng.shuffle(streams)
+    comp, blocks = _batch(streams, rng, out_skew=True)
+    got = engine_factory().bgzf_inflate(comp, blocks)
+    for (z, d), b in zip(streams, blocks):
+        assert got[int(b["uoff"]):int(b["uoff"]) + len(d)].tobytes() == d, (len(z), len(d))
+
+
+@pytest.mark.parametrize("case", ["truncated", "isize_small", "isize_large", "reserved", "oversubscribed"])
+def test_inflate_rejects_corrupt(engine_factory, case):
+    """One bad block among good ones is named by index (as zlib rejects it)."""
+    rng = random.Random(5)
+    good = [(D.deflate(x, 6, zlib.Z_DEFAULT_STRATEGY), x) for x in (rng.randbytes(3000), b"abc" * 900)]
+    d = rng.randbytes(5000) + b"xyz" * 500
+    z = D.deflate(d, 6, zlib.Z_DEFAULT_STRATEGY)
+    bad = {"truncated": (z[:-3], d), "isize_small": (z, d[:-1]), "isize_large": (z, d + b"!"),
+           "reserved": (bytes([0x07]) + z[1:], d),
+           "oversubscribed": (D.dynamic_block({8: 1, 1: 2, 2: 2}, [8] * 256 + [1], [1], b"SV"), b"SV")}[case]
+    if case == "oversubscribed":   # 256 x 2^-8 + 2^-1 > 1
+        assert not D.zlib_ok(*bad[:1], len(bad[1]))
+    comp, blocks = _batch(good + [bad] + good, rng)
+    with pytest.raises(RuntimeError, match="corrupt BGZF block 2"):
+        engine_factory().bgzf_inflate(comp, blocks)
 
 
 def test_inflate_mixed_streams(engine_factory):
@@ -92,13 +139,12 @@ def test_inflate_incomplete_codes_as_zlib(engine_factory):
     """Hand-built dynamic blocks on the device: an incomplete code-length code and
     an incomplete literal/length code are rejected as zlib rejects them (the host path and the
     reference's htslib inflate with zlib), a lone 1-bit distance code is accepted."""
-    from test_inflate_core import _dynamic_block, _zlib_ok
     data = b"SVTrek"
     eng = engine_factory()
     for cl, lit, valid in (({9: 1, 1: 2, 2: 2}, [9] * 256 + [1], True), ({9: 1, 1: 2}, [9] * 256 + [1], False),
                            ({9: 1, 2: 2, 1: 2}, [9] * 256 + [2], False)):
-        comp = _dynamic_block(cl, lit, [1], data)
-        assert _zlib_ok(comp, len(data)) == valid
+        comp = D.dynamic_block(cl, lit, [1], data)
+        assert D.zlib_ok(comp, len(data)) == valid
         blocks = np.array([(3, 0, len(comp), len(data))], dtype=BGZF_BLOCK_DTYPE)
         buf = bytes(3) + comp
         if valid:
