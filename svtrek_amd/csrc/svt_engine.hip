@@ -1718,7 +1718,10 @@ struct svt_ctx {
     // device index (svt_index.inc)
     uint64_t *d_part = nullptr;       // [n_ranges + 1]
     uint32_t n_ranges = 0;
-    IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan
+    IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan (first build: sizing)
+    uint4 *d_scr = nullptr;                        // stream walk: staged events / offsets per range, overflow flags
+    uint2 *d_scrh = nullptr;
+    uint32_t *d_ovf = nullptr;
     uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
     uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
     int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
@@ -1836,6 +1839,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_ins_off); hfree(c->d_ins_bases);
     hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
+    hfree(c->d_scr); hfree(c->d_scrh); hfree(c->d_ovf);
     c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
@@ -2174,11 +2178,20 @@ void parallel_for(size_t n, size_t cap, F fn) {
     for (auto &x : th) x.join();
 }
 
-// The device index of the loaded pileup (svt_index.inc / svt_index2.inc): census, exclusive
-// scan of the range (group) totals, emit.  `first`: size and allocate the event lists from the
-// totals (one synchronous read-back); later calls (svt_reindex) reuse them -- the totals depend
-// on the pileup only.  `ms`: the index kernels' device time (HIP events; the read-back and
-// allocations excluded).
+// The device index of the loaded pileup (svt_index.inc / svt_index2.inc).  Stream walk: the walk
+// (one pass over the stream, events staged per range), an exclusive scan of the range totals, the
+// staged rows to their places.  Lane per read: census, the scan of the group totals, emit.
+// `first`: between scan and placement, size and allocate the event lists from the totals (one
+// synchronous read-back); later calls (svt_reindex) reuse them -- the totals depend on the
+// pileup only.  `ms`: the index kernels' device time (HIP events; read-back and allocations
+// excluded).
+// lane per read (svt_index2.inc) for short reads -- a wave's 64 reads then take a few steps
+// each; long reads (a lane walking thousands of ops waits on its loads) take the stream walk,
+// which spreads every slot of 256 ops over the wave; never for a group of > 2^27 ops
+bool index_lane(const svt_ctx *c, uint64_t nops, uint64_t nreads) {
+    return c->n_groups > 0 && (c->ix_mode == 1 || (c->ix_mode == 0 && nops <= 64ull * nreads));
+}
+
 svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     IxArgs a;
     a.stream = c->d_cigar;
@@ -2194,6 +2207,9 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.capD = c->n_evD;
     a.capI = c->n_evI;
     a.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
+    a.scr = c->d_scr;
+    a.scrh = c->d_scrh;
+    a.ovf = c->d_ovf;
     a.n_ranges = c->n_ranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (ms)
@@ -2203,20 +2219,17 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
             if (e) (void)hipEventDestroy(e);
         return r;
     };
-    // lane per read (svt_index2.inc) for short reads -- a wave's 64 reads then take a few steps
-    // each; long reads (a lane walking thousands of ops waits on its loads) take the stream walk,
-    // which spreads every slot of 256 ops over the wave; never for a group of > 2^27 ops
-    const bool lane = c->n_groups > 0 && (c->ix_mode == 1 || (c->ix_mode == 0 && c->n_ops <= 64ull * c->n_reads));
+    const bool lane = index_lane(c, c->n_ops, (uint64_t)c->n_reads);
     c->load_stats.index_kind = lane ? 1u : 2u;
     const uint32_t nparts = lane ? c->n_groups : c->n_ranges;   // what the scan runs over
     Ix2Args a2{a, c->d_cnt, (uint64_t)c->n_reads, c->n_groups};
     const dim3 grid2((unsigned)((c->n_groups + IX2_WPB - 1) / IX2_WPB)), block2(64 * IX2_WPB);
+    const dim3 grid1((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block1(64 * IX_WPB);
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     if (lane)
         hipLaunchKernelGGL(ix2_census_kernel, grid2, block2, 0, st, a2);
     else
-        hipLaunchKernelGGL(ix_census_kernel, dim3((unsigned)((c->n_ranges + IXC_WPB - 1) / IXC_WPB)), dim3(64 * IXC_WPB), 0,
-                           st, a);
+        hipLaunchKernelGGL(index_kernel, grid1, block1, 0, st, a);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess)   // the ranges' / groups' exclusive prefixes
         e = hipcub::DeviceScan::ExclusiveScan(c->d_scan_tmp, c->scan_tmp_bytes, c->d_agg, c->d_wbase, IxTotSum(),
@@ -2247,7 +2260,7 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     }
     if (ms && hipEventRecord(ev[2], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     if (lane) hipLaunchKernelGGL(ix2_emit_kernel, grid2, block2, 0, st, a2);
-    else hipLaunchKernelGGL(index_kernel, dim3((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), dim3(64 * IX_WPB), 0, st, a);
+    else hipLaunchKernelGGL(ix_copy_kernel, grid1, block1, 0, st, a);
     e = hipGetLastError();
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index emit: %s", hipGetErrorString(e)));
     if (ms) {
@@ -2329,7 +2342,8 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
         for (int64_t r = tid_off[t], r1 = tid_off[t + 1]; r < r1;) {
             pt[t].push_back((uint64_t)r);
             const uint64_t s0 = soff[r];
-            for (r++; r < r1 && soff[r] - s0 < T; r++) {}
+            const int64_t rs = r;   // (at most IX_RCAP reads: the single-pass walk stages their offsets)
+            for (r++; r < r1 && soff[r] - s0 < T && r - rs < (int64_t)IX_RCAP; r++) {}
         }
     });
     std::vector<uint64_t> part;
@@ -2374,6 +2388,12 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
         c->scan_tmp_bytes = std::max<size_t>(need, 1);
     }
     if ((s = upload<uint64_t>(c, c->d_tot, nullptr, 0, IX_NTOT))) return s;
+    if (!index_lane(c, nops, (uint64_t)nr)) {   // the stream walk's scratch slots
+        const size_t RR = std::max<size_t>(c->n_ranges, 1);
+        if ((s = upload<uint4>(c, c->d_scr, nullptr, 0, RR * IX_SCAP))) return s;
+        if ((s = upload<uint2>(c, c->d_scrh, nullptr, 0, RR * IX_RCAP))) return s;
+        if ((s = upload<uint32_t>(c, c->d_ovf, nullptr, 0, RR))) return s;
+    }
     c->load_stats.upload_ms = ms_since(t_up);
     c->n_targets = nt;
     c->n_reads = nr;
@@ -2387,11 +2407,14 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
         c->load_stats.lead_blocks = 0;   // (no lead chunks since 0.17: refine_end's stops vote as e + 2)
         c->load_stats.slow_reads = 0;    // (no slow reads since 0.17: walks saturate at 2^30)
         // lane per read: census stream + soff + rec (24 B/read), cnt written (8 B/read); emit cnt
-        // + soff + rec (32 B/read) + stream, the per-read offsets (16 B/read) written.  Stream
-        // walk: census stream + rec (16 B/read); emit stream + soff + rec (24 B/read), offsets.
-        // Both: the events written.
-        const uint64_t per_read = c->load_stats.index_kind == 1 ? 80u : 56u;
-        c->load_stats.index_bytes = 8ull * nstream + per_read * R + 16ull * (c->n_evD + c->n_evI);
+        // + soff + rec (32 B/read) + stream, the per-read offsets (16 B/read) written; the events
+        // written.  Stream walk (one pass): stream + soff + rec (24 B/read); the staged offsets
+        // (8 B/read) and events written to scratch, read back, written to their places (16 B/read
+        // of offsets, 3 x 16 B/event).
+        if (c->load_stats.index_kind == 1)
+            c->load_stats.index_bytes = 8ull * nstream + 80ull * R + 16ull * (c->n_evD + c->n_evI);
+        else
+            c->load_stats.index_bytes = 4ull * nstream + 56ull * R + 48ull * (c->n_evD + c->n_evI);
     } else {
         for (auto *pp : {&c->d_spD, &c->d_spI})
             if ((s = upload<uint4>(c, *pp, nullptr, 0, 1))) return s;
