@@ -13,9 +13,9 @@ refines the g-th contiguous slice against only the reads its queries can reach
 A step is the whole per-locus path from the resident columnar pileup to refined calls:
   1. the device index build (svt_reindex: every read's CIGAR walked once,
      refinement.c:118-159/:184-221/:295-318): for short reads (cfg4) ix2_census_kernel +
-     ix2_emit_kernel, one lane per read; for long reads ix_census_kernel (a streaming
-     reduction) + index_kernel<emit> (the stream walk); a hipcub scan of the census totals
-     between the two),
+     ix2_emit_kernel, one lane per read, a hipcub scan of the census totals between them;
+     for long reads one pass over the stream: index_kernel (the stream walk, events staged
+     per range) + a hipcub scan of the range totals + ix_copy_kernel (the staged rows placed)),
   2. one batched refine launch over the rank's slice (svt_refine_device_records:
      refine_lane_kernel + refine_redo_kernel; loci and 16-B result records resident in HBM),
   3. at N > 1, the one collective of the path: an RCCL gather to rank 0 of the slice's 16-B
@@ -25,7 +25,8 @@ Rank 0 prints ONE JSON line.
 
 roofline (HBM-bound integer work, no MFMA): `achieved` = the step's algorithmic bytes -- what
 the engine's own algorithm must move: the index build's (svt_load_stats.index_bytes: the CIGAR
-stream twice, per-read records and offsets, the span events written) plus the refine launch's
+stream -- twice for the lane-per-read build, once for the stream walk --, per-read records and
+offsets, the span events written) plus the refine launch's
 (svt_work.event_bytes: loci, region queries, span bounds and events, 16-B result records) -- / the
 step's mean duration from HIP events on the launch stream; `frac` = achieved / 8 TB/s.
 `traffic` = the HBM bytes per step the rocprofv3 PMC passes of this engine version and workload
@@ -132,7 +133,7 @@ def _engine_version() -> str:
 
 
 STEP_KERNELS = ("ix2_census_kernel", "ix2_emit_kernel", "refine_lane_kernel", "refine_redo_kernel")
-STREAM_INDEX_KERNELS = ("ix_census_kernel", "index_kernel")   # the long-read index build (svt_index.inc)
+STREAM_INDEX_KERNELS = ("index_kernel", "ix_copy_kernel")   # the long-read index build (svt_index.inc)
 
 
 def _traffic(workload: str, records: bool) -> dict:
@@ -381,9 +382,11 @@ def main() -> int:
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "CIGAR stream twice (4 B/op; census + emit), per read 80 B (lane per "
-                                                "read: census soff, rec, counts; emit counts, soff, rec, offsets) or 56 B "
-                                                "(stream walk), 16 B/span event (svt_load_stats.index_bytes)",
+                             "index_bytes_def": "lane per read: CIGAR stream twice (4 B/op; census + emit), 80 B/read "
+                                                "(census soff, rec, counts; emit counts, soff, rec, offsets), 16 B/span "
+                                                "event; stream walk: the stream once, 56 B/read (soff, rec, staged and "
+                                                "placed offsets), 48 B/span event (staged, read back, placed) "
+                                                "(svt_load_stats.index_bytes)",
                          },
                          "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
                                           "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),

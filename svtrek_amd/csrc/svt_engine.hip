@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.17.0 (gfx950, index build by read length, span walk, lane vote, BGZF inflate)"
+#define SVT_VERSION "svtrek_amd 0.18.0 (gfx950, index build by read length / one-pass stream walk, span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 

@@ -37,8 +37,8 @@ STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's
            # index build is either the lane-per-read pair (short reads) or the stream walk (long reads)
     "ix2_census_kernel": "ix2_census_kernel",
     "ix2_emit_kernel": "ix2_emit_kernel",
-    "ix_census_kernel": "(anonymous namespace)::ix_census_kernel",
     "index_kernel": "(anonymous namespace)::index_kernel(",
+    "ix_copy_kernel": "ix_copy_kernel",
     "refine_lane_kernel": "refine_lane_kernel",
     "refine_redo_kernel": "refine_redo_kernel",
 }
