@@ -35,7 +35,7 @@ def engine_factory():
         """gather: "span" (span events through refine_lane_kernel<32> at every batch size -- the
         product picks it from 64K windows up), "span1" (one wave per
         window, refine_span_kernel: the product's pick for smaller batches) or "auto" (the product's
-        size-based pick).  env: extra engine switches read at svt_open (e.g. SVTREK_IX_EXACT=1)."""
+        size-based pick).  env: extra engine switches read at svt_open (e.g. SVTREK_IX=stream)."""
         g, lw = variants.get(gather, (gather, None))
         keys = ("SVTREK_GATHER", "SVTREK_LANE_W") + tuple(env or ())
         old = {k: os.environ.get(k) for k in keys}
