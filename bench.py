@@ -84,7 +84,7 @@ def cpu_cores() -> tuple[int, int, float | None]:
     return n, aff, quota
 
 
-def cpu_baseline(res, loci, n_threads: int, budget_s: float = 24.0) -> dict:
+def cpu_baseline(res, loci, n_threads: int, budget_s: float = 24.0, sample_loci: int = 1000) -> dict:
     """Time the CPU oracle (reference-shaped restatement, T pthread workers) on a bounded
     sample of the same workload.  Test-infrastructure leg: the only bench use of oracle/."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -120,7 +120,7 @@ def cpu_baseline(res, loci, n_threads: int, budget_s: float = 24.0) -> dict:
     # the BGZF leg: per-thread BAM handle + BAI, per-query linear-index seek,
     # block inflate and record decode, as the reference's htslib calls do -- the baseline value
     import bgzf_baseline as BB  # noqa: E402
-    out.update(BB.run(res, loci, n_threads, budget_s=budget_s))
+    out.update(BB.run(res, loci, n_threads, budget_s=budget_s, k=sample_loci))
     if "value_bgzf" in out:
         out["value"] = out["value_bgzf"]
         out["sample"] = out["bgzf_sample"] + "; in-memory leg (no BGZF): " + out["sample"]
@@ -160,6 +160,9 @@ def main() -> int:
     ap.add_argument("--no-cold", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records check")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-sample-loci", type=int, default=1000,
+                    help="loci of the BGZF CPU leg's sample (the first K of contig 1, genomic order; 45000 ~ cfg4's "
+                         "whole contig 1 -- the bytes tools/e2e_bench.py --region-sample K writes)")
     ap.add_argument("--emulate-shard", default=None, metavar="N:R",
                     help="diagnostic, one process: run rank R's slice of an N-GPU run (its loci and halo reads) "
                          "alone -- the per-rank work of the multi-GPU bench, measured on one GPU")
@@ -328,7 +331,7 @@ def main() -> int:
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores, aff, quota = cpu_cores()
-        cpu = cpu_baseline(res, sl, args.cpu_threads or cores)
+        cpu = cpu_baseline(res, sl, args.cpu_threads or cores, sample_loci=args.cpu_sample_loci)
         cpu["affinity_cpus"] = aff
         cpu["cgroup_cpu_quota"] = quota
 
