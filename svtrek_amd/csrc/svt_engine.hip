@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.18.0 (gfx950, index build by read length / one-pass stream walk, span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.19.0 (gfx950, index build by read length / one-pass stream walk with light slots, span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -128,27 +128,8 @@ constexpr size_t CTL_REDO = 200;    // two redo counters (alternating launches)
 static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
 
 // ------------------------------------------------------------------ wave primitives
-#ifndef SVT_COLD_NOINLINE
-#define SVT_COLD_NOINLINE 0
-#endif
-#if SVT_COLD_NOINLINE
-#define SVT_COLD __noinline__
-#else
-#define SVT_COLD __forceinline__
-#endif
-#ifndef SVT_OPAQUE_LANE
-#define SVT_OPAQUE_LANE 0
-#endif
-// The lane id behind an empty volatile asm: lane-dependent values (the sort networks'
-// exchange masks, ...) are then recomputed where used instead of being hoisted out of the
-// batched kernel's per-window loop and held live across it (VGPR/SGPR pressure).
-__device__ __forceinline__ int lane_id() {
-    int l = (int)__lane_id();
-#if SVT_OPAQUE_LANE
-    asm volatile("" : "+v"(l));
-#endif
-    return l;
-}
+#define SVT_COLD __forceinline__   // (cold paths inlined: out-of-line calls measured slower)
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 // The lane mask of p straight from its compare (no v_cndmask / v_cmp round trip through a VGPR).
 __device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
@@ -664,9 +645,6 @@ struct Band {
     int32_t lo = 0, hi = 0;   // the band: open interval (lo, hi)
 };
 
-#ifndef SVT_BAND
-#define SVT_BAND 1
-#endif
 // Compacts buf[0..n) (n <= 4*WAVE) to its band elements in place; returns their count.
 // Counts only (ballots), no reductions; int32 compares throughout, since the band is only
 // used when |pos| < 2^30 and range + max(ci, 0) <= 2^22 (so lo, hi fit) and every element
@@ -915,7 +893,7 @@ __device__ __forceinline__ int32_t sort_and_vote(int32_t *buf, int64_t *P, int32
     const int ln = lane_id();
     Band bd;
     if (given) bd = *given;   // buf already holds the band (band_filter_large)
-    else if (!LARGE && VOTE == V_CONSENSUS && SVT_BAND && n <= 4 * WAVE) n = band_filter(buf, n, pos, k, bd);
+    else if (!LARGE && VOTE == V_CONSENSUS && n <= 4 * WAVE) n = band_filter(buf, n, pos, k, bd);
     int32_t x0 = 0;   // sorted element ln, from the register sorts (no LDS read-back below)
     if (LARGE) {
         int N = 1;
@@ -1042,7 +1020,7 @@ __device__ __forceinline__ int32_t vote_window(const KArgs &a, WinLds &lds, int 
     WinStats st2;
     Sink s2{g, N, &lds.ncand};
     gather<KIND, false, G>(a, chrom - 1, s, e, s2, st2, lds);
-    if (VOTE == V_CONSENSUS && SVT_BAND) {   // the exact band first: usually small enough for the register sort
+    if (VOTE == V_CONSENSUS) {   // the exact band first: usually small enough for the register sort
         Band bd;
         const int32_t nb = band_filter_large(g, n, (int32_t)imprecise, a.prm, bd);
         if (bd.on && nb <= CAP) {
@@ -1059,40 +1037,17 @@ __device__ __forceinline__ int32_t vote_window(const KArgs &a, WinLds &lds, int 
 // g's first window (DEL: refine_start over [pos-wider, pos+narrow], INS: refine_ins),
 // window n + i is locus i's second (DEL: refine_end over end +- narrow): the wide windows
 // are dispatched first, so the short ones fill the tail.
+// (Workgroups in dispatch order: an XCD-aware swizzle -- each XCD a contiguous run of
+// neighbouring loci -- measured slower, 37.1 vs 35.3 us on cfg2: the launch's records stay in
+// the MALL across launches, so L2 locality buys nothing.)
 constexpr int WPB = 4;
-#ifndef SVT_INTERLEAVE_WINDOWS
-#define SVT_INTERLEAVE_WINDOWS 0
+#ifndef SVT_LANE16_WINDOWS
+#define SVT_LANE16_WINDOWS (1 << 19)
 #endif
-// XCD-aware workgroup order: blocks dispatch round-robin over the 8 XCDs (each with its own
-// L2); the swizzle gives every XCD a contiguous run of workgroups -- neighbouring loci, whose
-// windows share reads -- separately within each half of the dispatch order (so the wide
-// first windows still go first).  Bijective for any grid (MI355X guide, T1).  Off: measured
-// slower on cfg2 (37.1 vs 35.3 us) -- the launch's ~80 MB of records stay in the MALL across
-// launches, so L2 locality buys nothing and the reordered dispatch costs balance.
-#ifndef SVT_XCD_SWIZZLE
-#define SVT_XCD_SWIZZLE 0
-#endif
-__device__ __forceinline__ uint32_t xcd_swz(uint32_t o, uint32_t nwg) {
-    const uint32_t x = o % 8u, q = nwg / 8u, r = nwg % 8u;
-    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + o / 8u;
-}
-__device__ __forceinline__ uint32_t window_block() {
-    const uint32_t b = blockIdx.x;
-    if (!SVT_XCD_SWIZZLE) return b;
-    const uint32_t nwg = gridDim.x, na = (nwg / 2u) & ~7u;
-    return b < na ? xcd_swz(b, na) : na + xcd_swz(b - na, nwg - na);
-}
 
-// The timed index-walk kernel is held to 64 VGPRs = 8 waves per SIMD (the CU's maximum):
-// the walk is bound by dependent-load latency, so resident waves are what hide it.
-#ifndef SVT_WAVES_PER_EU
-#define SVT_WAVES_PER_EU 8
-#endif
-#if SVT_WAVES_PER_EU
-#define SVT_OCC __attribute__((amdgpu_waves_per_eu(SVT_WAVES_PER_EU, SVT_WAVES_PER_EU)))
-#else
-#define SVT_OCC
-#endif
+// The refine kernels are held to 64 VGPRs = 8 waves per SIMD (the CU's maximum): their walks
+// are bound by dependent-load latency, so resident waves are what hide it.
+#define SVT_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
 template <bool COUNT, int G>
 __device__ __forceinline__ void refine_body(const KArgs &a);
 
@@ -1132,21 +1087,14 @@ __device__ __forceinline__ int32_t gather_window(const KArgs &a, WinLds &lds, in
     return n;
 }
 
-#ifndef SVT_SHARED_VOTE
-#define SVT_SHARED_VOTE 1
-#endif
 template <bool COUNT, int G>
 __device__ __forceinline__ void refine_body(const KArgs &a) {
     __shared__ WinLds lds_all[WPB];
     const uint32_t wid = threadIdx.x >> 6;
-    const uint32_t g = window_block() * WPB + wid;
+    const uint32_t g = blockIdx.x * WPB + wid;
     if (g >= 2 * a.n) return;
     WinLds &lds = lds_all[wid];
-#if SVT_INTERLEAVE_WINDOWS
-    const uint32_t w = g & 1u, li = g >> 1;      // a locus' two windows back to back (L2/MALL reuse)
-#else
     const uint32_t w = g >= a.n ? 1u : 0u, li = g - w * a.n;
-#endif
     const svt_locus L = a.loci[li];
     const int32_t type = uniform_i(L.type), chrom = uniform_i(L.chrom);
     const uint32_t pos = (uint32_t)uniform_i((int32_t)L.pos), end = (uint32_t)uniform_i((int32_t)L.end);
@@ -1164,12 +1112,6 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
         else { kind = K_END; s = end - (uint32_t)k.narrow; e = end + (uint32_t)k.narrow; imp = end; }
     }
     uint32_t r = SVT_NA;
-#if !SVT_SHARED_VOTE
-    int32_t sup = 0;
-    if (kind == K_INS) r = (uint32_t)refine_window<K_INS, COUNT, G>(a, lds, chrom, s, e, imp, wk, sup);
-    else if (kind == K_START) r = (uint32_t)refine_window<K_START, COUNT, G>(a, lds, chrom, s, e, imp, wk, sup);
-    else if (kind == K_END) r = (uint32_t)refine_window<K_END, COUNT, G>(a, lds, chrom, s, e, imp, wk, sup);
-#else
     if (kind >= 0) {
         // the kind-specific gathers, then ONE copy of the sort + vote for all kinds (code size:
         // the three inlined copies of the vote no longer compete for the instruction cache)
@@ -1186,7 +1128,6 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
         else if (kind == K_START) r = (uint32_t)vote_window<K_START, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
         else r = (uint32_t)vote_window<K_END, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
     }
-#endif
     if (lane_id() == 0) {
         write_result(a, li, w, r);
         if (COUNT)
@@ -1425,9 +1366,6 @@ __device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &l
     return -1;
 }
 
-#ifndef SVT_LANE_VOTE
-#define SVT_LANE_VOTE 1
-#endif
 
 // One window's A2 + A3 answer, computed by one lane (phase 0).  u32 words only (the rows
 // it is parked in are 4-byte aligned).
@@ -1503,7 +1441,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     const KParams &k = a.prm;
     const uint32_t cnt = min((uint32_t)LV_W, nw - g0);
     const int32_t bw = k.range + max(k.ci, 0);   // the band's half-width
-    const bool band_ok = k.range > SV_MIN_LENGTH / 2 && bw <= LV_WMAX && k.ci >= -LV_WMAX && SVT_LANE_VOTE &&
+    const bool band_ok = k.range > SV_MIN_LENGTH / 2 && bw <= LV_WMAX && k.ci >= -LV_WMAX &&
                          SVT_DIAG != 7;
     // ---- phase 0: every window's A2 + A3 at once, one lane each (the dependent loads of
     // locus -> bucket words -> pos/emax searches -> span bounds run once per LV_W windows),
@@ -1523,7 +1461,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         return;
     }
-    // ---- phase 1: span walk + band per window (wave-wide)
+    // ---- phase 1: span walk + band per window (wave-wide).  (Loading the first 64-256 events
+    // of window kw + 1's span before window kw is walked measured 6-9 % slower on cfg4:
+    // profiles/r04_ab2 -- the walk is issue-bound, not latency-bound.)
     for (uint32_t kw = 0; kw < cnt; kw++) {
         const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.stage + kw * LV_S);
         const int32_t qk = uniform_i(qp->kind);
@@ -1699,7 +1639,8 @@ struct svt_ctx {
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
     uint64_t ix_ranges = 65536;   // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
-    int lane_w = 0;               // SVTREK_LANE_W=32 forces the lane kernel at every batch size (tests)
+    int lane_w = 0;               // SVTREK_LANE_W=32 / 16 force the lane kernel, that many windows a wave, at
+                                  // every batch size (tests)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
     uint32_t lane_par = 0;        // which of the two redo counters the next lane launch uses
@@ -1916,8 +1857,14 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
         a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + c->lane_par;
         a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->lane_par ^ 1u);
         c->lane_par ^= 1u;
-        hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
-                           st, a);
+        // 32 windows a wave; 16 below LANE16_WINDOWS windows, where 32 a wave leaves the chip's
+        // 8192 wave slots underfilled (a 125K-locus shard of the 8-GPU run: 250K windows, ~7.8K waves)
+        if (c->lane_w == 16 || (c->lane_w == 0 && 2 * n < (size_t)SVT_LANE16_WINDOWS))
+            hipLaunchKernelGGL(refine_lane_kernel<16>, dim3((unsigned)((2 * n + WPB * 16 - 1) / (WPB * 16))), block, 0,
+                               st, a);
+        else
+            hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
+                               st, a);
         hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
     } else {
         hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
@@ -2107,7 +2054,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *x = getenv("SVTREK_IX")) c->ix_mode = strcmp(x, "lane") == 0 ? 1 : strcmp(x, "stream") == 0 ? 2 : 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
-    if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 32 ? 32 : 0;
+    if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 32 ? 32 : atoi(lw) == 16 ? 16 : 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;
