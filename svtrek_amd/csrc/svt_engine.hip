@@ -1041,9 +1041,6 @@ __device__ __forceinline__ int32_t vote_window(const KArgs &a, WinLds &lds, int 
 // neighbouring loci -- measured slower, 37.1 vs 35.3 us on cfg2: the launch's records stay in
 // the MALL across launches, so L2 locality buys nothing.)
 constexpr int WPB = 4;
-#ifndef SVT_LANE16_WINDOWS
-#define SVT_LANE16_WINDOWS (1 << 19)
-#endif
 
 // The refine kernels are held to 64 VGPRs = 8 waves per SIMD (the CU's maximum): their walks
 // are bound by dependent-load latency, so resident waves are what hide it.
@@ -1639,8 +1636,7 @@ struct svt_ctx {
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
     uint64_t ix_ranges = 65536;   // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
-    int lane_w = 0;               // SVTREK_LANE_W=32 / 16 force the lane kernel, that many windows a wave, at
-                                  // every batch size (tests)
+    int lane_w = 0;               // SVTREK_LANE_W=32 forces the lane kernel at every batch size (tests)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
     uint32_t lane_par = 0;        // which of the two redo counters the next lane launch uses
@@ -1857,14 +1853,10 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
         a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + c->lane_par;
         a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->lane_par ^ 1u);
         c->lane_par ^= 1u;
-        // 32 windows a wave; 16 below LANE16_WINDOWS windows, where 32 a wave leaves the chip's
-        // 8192 wave slots underfilled (a 125K-locus shard of the 8-GPU run: 250K windows, ~7.8K waves)
-        if (c->lane_w == 16 || (c->lane_w == 0 && 2 * n < (size_t)SVT_LANE16_WINDOWS))
-            hipLaunchKernelGGL(refine_lane_kernel<16>, dim3((unsigned)((2 * n + WPB * 16 - 1) / (WPB * 16))), block, 0,
-                               st, a);
-        else
-            hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
-                               st, a);
+        // (16 windows a wave for the 250K-window launches of a 125K-locus shard measured slower:
+        // 0.132-0.138 vs 0.117-0.121 ms, profiles/r04_sh)
+        hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
+                           st, a);
         hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
     } else {
         hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
@@ -2054,7 +2046,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     c->lane_vote = !(g && strcmp(g, "span1") == 0);
     if (const char *x = getenv("SVTREK_IX")) c->ix_mode = strcmp(x, "lane") == 0 ? 1 : strcmp(x, "stream") == 0 ? 2 : 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
-    if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 32 ? 32 : atoi(lw) == 16 ? 16 : 0;
+    if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 32 ? 32 : 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;

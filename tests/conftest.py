@@ -29,12 +29,11 @@ def engine_factory():
     engines = []
 
     # gather variant -> (SVTREK_GATHER, SVTREK_LANE_W)
-    variants = {"span": ("span", "32"), "lane16": ("span", "16"), "auto": ("span", None), "span1": ("span1", None)}
+    variants = {"span": ("span", "32"), "auto": ("span", None), "span1": ("span1", None)}
 
     def make(params=None, gather="span", env=None):
         """gather: "span" (span events through refine_lane_kernel<32> at every batch size -- the
-        product picks it from 512K windows up), "lane16" (refine_lane_kernel<16> at every batch
-        size: the product's pick from 64K to 512K windows), "span1" (one wave per
+        product picks it from 64K windows up), "span1" (one wave per
         window, refine_span_kernel: the product's pick for smaller batches) or "auto" (the product's
         size-based pick).  env: extra engine switches read at svt_open (e.g. SVTREK_IX=stream)."""
         g, lw = variants.get(gather, (gather, None))

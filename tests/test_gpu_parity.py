@@ -38,7 +38,7 @@ def test_consensus_vectors_through_kernel(engine_factory):
         assert int(O.refine_batch(pl, loci)["start"][0]) == exp
 
 
-@pytest.mark.parametrize("gather", ["span", "lane16", "span1"])
+@pytest.mark.parametrize("gather", ["span", "span1"])
 @pytest.mark.parametrize("seed", range(6))
 def test_random_consensus_windows(engine_factory, seed, gather):
     rng = np.random.default_rng(seed)
@@ -62,7 +62,7 @@ def test_random_consensus_windows(engine_factory, seed, gather):
     _assert_same(got, want, loci)
 
 
-@pytest.mark.parametrize("gather", ["span", "lane16", "span1"])
+@pytest.mark.parametrize("gather", ["span", "span1"])
 @pytest.mark.parametrize("seed", range(10))
 def test_fuzz_pileups(engine_factory, seed, gather):
     rng = np.random.default_rng(1000 + seed)
@@ -234,7 +234,7 @@ def test_repeatability_and_batch_split(engine_factory):
     assert (c == a).all()
 
 
-@pytest.mark.parametrize("gather", ["span", "lane16", "span1"])
+@pytest.mark.parametrize("gather", ["span", "span1"])
 def test_hifi_short_cigars(engine_factory, gather):
     """HiFi-like: ~30 ops per read, many reads per 256-op index slot (read starts mid-lane)."""
     cfg = sim.SimConfig(seed=12, n_targets=2, n_loci=600, del_frac=0.5, coverage=30, read_len_mean=15000,
@@ -394,7 +394,7 @@ def test_hip_and_cpu_backends_through_one_abi(engine_factory, seed):
             (wg["windows"], wg["reads"], wg["ops_walked"], wg["candidates"])
 
 
-@pytest.mark.parametrize("gather", ["span", "lane16", "span1"])
+@pytest.mark.parametrize("gather", ["span", "span1"])
 @pytest.mark.parametrize("nsplit", [20, 90, 300])
 def test_lane_kernel_split_reads_bands_and_left_overs(engine_factory, nsplit, gather):
     """refine_end over many split reads (leading S, walk past the window end: the LEAD/TRAIL
