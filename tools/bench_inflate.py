@@ -1,4 +1,4 @@
-"""BGZF inflate throughput: the device kernel (svt_bgzf_inflate, one lane per block) vs the
+"""BGZF inflate throughput: the device kernel (svt_bgzf_inflate, one wave per block) vs the
 host (zlib on T threads, the same per-block inflate the host ingest runs), on a BAM with
 SEQ/QUAL written by the simulator.  Prints one JSON line.
 
