@@ -40,6 +40,7 @@ STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's
     "index_kernel": "(anonymous namespace)::index_kernel(",
     "ix_copy_kernel": "ix_copy_kernel",
     "refine_lane_kernel": "refine_lane_kernel",
+    "refine_span_kernel": "refine_span_kernel",   # (the engine's pick below 64K windows: cfg1, cfg2)
     "refine_redo_kernel": "refine_redo_kernel",
 }
 
