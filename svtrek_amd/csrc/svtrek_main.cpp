@@ -282,7 +282,10 @@ struct DeviceDecode {
     svt_ctx **ctx;
     const int *open_rc;
     svt_bam_dec *dec = nullptr;
-    bool pinned = true;   // batch buffers in pinned host memory (SVTREK_DEC_PINNED=0: pageable)
+    // batch buffers in pageable host memory (SVTREK_DEC_PINNED=1: pinned).  Pinning two 256 MiB
+    // buffers is on every run's critical path and costs more than the runtime's staged copies of
+    // pageable memory: cfg4 contig 1.13-1.34 s pageable vs 1.54-1.60 s pinned (profiles/r04_batch2)
+    bool pinned = false;
 };
 int dd_begin(void *user, int32_t n_targets, char *err, size_t ecap) {
     DeviceDecode *d = (DeviceDecode *)user;
@@ -349,7 +352,10 @@ int audit(int argc, char **argv) {
     // GPU inflate: 1 GiB compressed batches (~21K BGZF blocks, one lane each; larger batches
     // inflate faster but pinning their buffers costs more: cfg2 e2e 5.4 s at 1 GiB, 9.0 s at 4 GiB)
     size_t batch_mb = 1024;
-    if (const char *x = getenv("SVTREK_INFLATE_BATCH_MB")) batch_mb = std::max<size_t>(1, strtoull(x, nullptr, 10));
+    // the device record decode: 256 MiB batches (pinned buffers: cfg4 contig 1 1.51 s at 256 MiB,
+    // 1.79 at 512, 2.09 at 1 GiB, 1.54 / 1.82 at 128 / 64; cfg2 2.66 / 2.72 / 3.36 s; profiles/r04_batch*)
+    size_t dec_batch_mb = 256;
+    if (const char *x = getenv("SVTREK_INFLATE_BATCH_MB")) dec_batch_mb = batch_mb = std::max<size_t>(1, strtoull(x, nullptr, 10));
     const svth_inflater dev_inf{device_inflate, device_host_alloc, device_host_free, &dinf, batch_mb << 20};
     // one GPU: the records are decoded on the device too (svt_bam_dec_*; SVTREK_HOSTPARSE=1: the
     // device inflates, the host parses, as for --gpus N > 1)
@@ -357,7 +363,7 @@ int audit(int argc, char **argv) {
     const bool dev_decode = a.gpu_inflate && G == 1 && !(hp && atoi(hp) == 1);
     DeviceDecode ddec{dinf.ready, &ctxs[0], &open_rc[0]};
     if (const char *x = getenv("SVTREK_DEC_PINNED")) ddec.pinned = atoi(x) != 0;
-    const svth_dev_sink dsink{dd_begin, dd_feed, dd_alloc, dd_release, &ddec, batch_mb << 20};
+    const svth_dev_sink dsink{dd_begin, dd_feed, dd_alloc, dd_release, &ddec, dec_batch_mb << 20};
     svth_bam *bam = nullptr;
     double dstage[4] = {0, 0, 0, 0};
     int dec_rc = 0;
