@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.19.1 (gfx950, index build by read length / one-pass stream walk with light slots, span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.20.0 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -1635,7 +1635,7 @@ struct svt_ctx {
     svt_params prm{};
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
-    uint64_t ix_ranges = 65536;   // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
+    uint64_t ix_ranges = 131072;  // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
     int lane_w = 0;               // SVTREK_LANE_W=32 forces the lane kernel at every batch size (tests)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
