@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.20.0 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.21.0 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -1171,10 +1171,28 @@ constexpr uint32_t LV_NONE = 1u << 14;   // no window (INV / other types): NA
 #define LV_WHY(r) 0u
 #endif
 
+#ifndef SVT_PACK
+#define SVT_PACK 1
+#endif
+// Phase 1's packed walk (SVT_PACK): the windows with a span to walk, in wave order, one entry
+// each (written by their phase-0 lanes); consecutive windows of <= 64 events together share
+// one 64-event slot.
+struct alignas(16) LvWin {
+    uint64_t e0;    // the span's first event
+    uint32_t s, e;  // the window
+    int32_t lo;     // the band's low end
+    uint32_t kl;    // kind | the window's lane (row) << 8
+    uint32_t len;   // span events (> 0)
+    uint32_t pad;
+};
+
 template <int W>
 struct LaneLds {
     uint16_t stage[W * LV_S];   // parked queries (phase 0 -> 1), band offsets (1 -> 2)
     LvMeta meta[W];
+#if SVT_PACK
+    LvWin win[W];
+#endif
 };
 
 // Phase 1 of one window, wave-wide (A4-A7 + the band): the window's span events [E0, E0+len)
@@ -1255,6 +1273,48 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
         }
     }
     return LaneBand{n, nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
+}
+
+// One 64-event slot holding the whole spans of consecutive walkable windows win[c0..]: bit i of
+// M marks the first lane of a window (bit 0 always), tot <= 64 events in all.  Lane j walks
+// event j - f of the window that starts at f = the highest mark <= j, with that window's own
+// s / e / band (the tests of span_cand_mask, per lane); members go to the window's row at
+// their rank among its members, and each window's first lane writes its meta row (band size,
+// candidates, below / above) -- everything lane_walk gives a window, for 1-64 events at once.
+__device__ __forceinline__ void lane_packed(const DevPileup &P, const LvWin *win, LvMeta *meta, uint16_t *stage,
+                                            uint32_t c0, uint64_t M, uint32_t tot, int32_t bw2) {
+    const int ln = lane_id();
+    const uint64_t upto = M & ((2ull << ln) - 1ull);   // marks at or below this lane (ln 63: all)
+    const uint32_t r = (uint32_t)__popcll(upto) - 1u, f = 63u - (uint32_t)__clzll(upto);
+    const LvWin w = win[c0 + r];
+    const uint32_t kind = w.kl & 0xffu, k = w.kl >> 8;
+    const uint4 *evb = (kind == (uint32_t)K_INS ? P.spI : P.spD) + w.e0;
+    const uint4 v = evb[min((uint32_t)ln - f, w.len - 1u)];   // lanes past tot: their window's last event
+    const uint32_t s = w.s, e = w.e, x = v.x, op = v.y & 0xfu;
+    const int32_t lo = w.lo;
+    const uint64_t base = ballot((uint32_t)ln < tot) & ballot((int32_t)v.z > (int32_t)(s - 1u)) & ballot(x <= e);
+    const uint64_t isI = ballot(kind == (uint32_t)K_INS), isE = ballot(kind == (uint32_t)K_END);
+    const uint64_t oD = ballot(op == OP_DEL), sx = ballot(s <= x);
+    const uint64_t lead = base & isE & ballot(op == SP_LEAD) & sx;   // refinement.c:210-220
+    const uint64_t brk = lead & ballot(v.w > e);
+    const uint64_t cm = (base & ((isI & ballot(op == OP_INS)) | (~(isI | isE) & (oD | (ballot(op == SP_TRAIL) & sx))) |
+                                 (isE & oD))) |
+                        (lead & ~brk);
+    const int32_t iv = (int32_t)(kind == (uint32_t)K_END ? (op == OP_DEL ? x + (v.y >> 4) + 1u : v.w + 1u) : x);
+    const uint64_t gt = ballot(iv > lo), lt = ballot(iv < lo + bw2);
+    const uint64_t mb = cm & gt & lt;
+    if ((mb >> ln) & 1ull) {
+        const uint32_t rank = mbcnt(mb) - (uint32_t)__popcll(mb & ((1ull << f) - 1ull));
+        stage[k * LV_S + min(rank, (uint32_t)LV_CAP)] = (uint16_t)(iv - lo);
+    }
+    if ((M >> ln) & 1ull) {   // the window's first lane: its totals over lanes [ln, ln + len)
+        const uint64_t rm = (w.len >= 64u ? ~0ull : ((1ull << w.len) - 1ull)) << ln;
+        const uint32_t nb = (uint32_t)__popcll(mb & rm);
+        const bool below = (cm & ~gt & rm) != 0ull, above = ((brk | (cm & ~lt)) & rm) != 0ull;
+        meta[k].flags = nb > (uint32_t)LV_CAP ? (LV_REDO | LV_WHY(3))
+                                              : nb | LV_PENDING | (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u);
+        meta[k].n = (int32_t)__popcll((cm | brk) & rm);
+    }
 }
 
 template <int N>
@@ -1443,6 +1503,39 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     // ---- phase 0: every window's A2 + A3 at once, one lane each (the dependent loads of
     // locus -> bucket words -> pos/emax searches -> span bounds run once per LV_W windows),
     // parked in the window's staging row (read back before that row is written)
+#if SVT_PACK
+    // (packed: the meta row gets its final flags here unless the window has a span to walk,
+    // and the walkable windows' table entries go to win[] in lane order)
+    uint32_t nwin;
+    {
+        const bool mine = (uint32_t)ln < cnt;
+        LvQuery q{};
+        if (mine) lane_query(a, g0 + (uint32_t)ln, band_ok, q);
+        const bool walk = mine && q.kind >= 0 && !(q.kind & LQ_REDO) && q.len != 0u;
+        if (mine) {
+            LvMeta m;
+            m.lo = q.lo;
+            m.liw = q.liw;
+            m.flags = q.kind < 0 ? LV_NONE : (q.kind & LQ_REDO) ? (LV_REDO | LV_WHY(1)) : LV_PENDING;
+            m.n = 0;
+            L.meta[ln] = m;
+        }
+        const uint64_t wm = ballot(walk);
+        if (walk) {
+            LvWin wn;
+            wn.e0 = (uint64_t)q.e0[0] | (uint64_t)q.e0[1] << 32;
+            wn.s = q.s;
+            wn.e = q.e;
+            wn.lo = q.lo;
+            wn.kl = (uint32_t)q.kind | (uint32_t)ln << 8;
+            wn.len = q.len;
+            wn.pad = 0u;
+            L.win[mbcnt(wm)] = wn;
+        }
+        nwin = (uint32_t)__popcll(wm);
+    }
+    wave_sync();
+#else
     if ((uint32_t)ln < cnt) {
         LvQuery q{};
         lane_query(a, g0 + (uint32_t)ln, band_ok, q);
@@ -1451,6 +1544,48 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         L.meta[ln].liw = q.liw;   // phase 1 adds flags and n
     }
     wave_sync();
+#endif
+#if SVT_PACK
+    // ---- phase 1 (packed): windows of <= 64 events share slots (lane_packed), longer ones are
+    // walked alone (lane_walk); their lengths sit in a VGPR, read by the scalar loop
+    {
+        const uint32_t lenv = (uint32_t)ln < nwin ? L.win[ln].len : 0u;
+        for (uint32_t c = 0; c < nwin;) {
+            const uint32_t l0 = rdlane(lenv, (int)c);
+            if (l0 > (uint32_t)WAVE) {
+                const LvWin *wp = &L.win[c];
+                const uint32_t kl = (uint32_t)uniform_i((int32_t)wp->kl);
+                const uint32_t s = (uint32_t)uniform_i((int32_t)wp->s), e = (uint32_t)uniform_i((int32_t)wp->e);
+                const int32_t lo = uniform_i(wp->lo);
+                const uint64_t E0 = (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)wp->e0) |
+                                    (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)(wp->e0 >> 32)) << 32;
+                const uint32_t kind = kl & 0xffu, kw = kl >> 8;
+                uint16_t *row = L.stage + kw * LV_S;
+                LaneBand r;
+                if (kind == (uint32_t)K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, l0, lo, lo + 2 * bw, row);
+                else if (kind == (uint32_t)K_START) r = lane_walk<K_START>(a.pile, s, e, E0, l0, lo, lo + 2 * bw, row);
+                else r = lane_walk<K_END>(a.pile, s, e, E0, l0, lo, lo + 2 * bw, row);
+                if (ln == 0) {
+                    L.meta[kw].flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : (uint32_t)r.nb | LV_PENDING | r.flags;
+                    L.meta[kw].n = r.n;
+                }
+                c++;
+                continue;
+            }
+            uint64_t M = 1ull;
+            uint32_t tot = l0, c1 = c + 1u;
+            for (; c1 < nwin; c1++) {
+                const uint32_t l = rdlane(lenv, (int)c1);
+                if (tot + l > (uint32_t)WAVE) break;
+                M |= 1ull << tot;
+                tot += l;
+            }
+            lane_packed(a.pile, L.win, L.meta, L.stage, c, M, tot, 2 * bw);
+            c = c1;
+        }
+        wave_sync();
+    }
+#else
     if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
         if ((uint32_t)ln < cnt) {
             const LvQuery q = *reinterpret_cast<const LvQuery *>(L.stage + (uint32_t)ln * LV_S);
@@ -1493,6 +1628,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
+#endif
     if (SVT_DIAG == 8) {   // diagnostic build: phases 0-1 only (a checksum of their LDS output written out)
         if ((uint32_t)ln < cnt) {
             const LvMeta mt = L.meta[ln];
