@@ -149,9 +149,125 @@ def _traffic(workload: str, records: bool) -> dict:
             and bool(e.get("records", False)) == records}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start N fresh rank processes
+    (this script again, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each) and wait.
+
+    The parent makes no torch / HIP call (it never imports torch), so the ranks are children,
+    not an exec of a process that touched the GPU. Rank 0 prints the one JSON line (the
+    children share this process's stdout). If any rank exits non-zero the others are
+    terminated (by their own PIDs) and the first failing status is returned. This is the
+    fan-out of the reference's T tpool workers (audit.c:287-293), one process per GPU."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with status {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return status
+
+
+def dry_run(args, world: int, rank: int) -> int:
+    """`--dry-run`: the N-rank plumbing of the bench on the CPU (gloo), no engine. Each rank
+    shards the seeded workload exactly as the GPU run does, writes its slice's 16-B records
+    (the loci unrefined: start = end = NA) into the double-buffered gather for K steps, and
+    rank 0 checks that every VCF row arrived exactly once and prints the one JSON line. It
+    measures nothing (value is the plumbing's own rate) -- it exists so that the launcher, the
+    rank environment and the gather are exercised without a GPU (tests/test_distributed.py)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from svtrek_amd import Params, sim
+    from svtrek_amd._lib import RECORD_DTYPE, RESULT_DTYPE, SVT_NA
+    from svtrek_amd.distributed import PipelinedGather, pack_records, padded_rows, shard_workload, unpack_records
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    cfg = sim.WORKLOADS[args.workload]
+    if args.scale != 1.0:
+        from dataclasses import replace
+        cfg = replace(cfg, n_loci=max(1, int(cfg.n_loci * args.scale)))
+    res = sim.generate(cfg)
+    rows, sl, spile = shard_workload(res.loci, res.pileup, Params(), world, rank)
+    n_total, per = len(res.loci), padded_rows(len(res.loci), world)
+    local = np.zeros(len(sl), dtype=RESULT_DTYPE)
+    local["start"] = SVT_NA
+    local["end"] = SVT_NA
+    recs = torch.from_numpy(pack_records(rows, local, per).view(np.int32).reshape(-1).copy())
+    pg = PipelinedGather(lambda: torch.full((per * RECORD_DTYPE.itemsize // 4,), -1, dtype=torch.int32),
+                         world, rank, enabled=world > 1)
+    for i in range(args.warmup):
+        pg.buffer(i).copy_(recs)
+        pg.submit(i)
+    pg.drain()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        pg.buffer(i).copy_(recs)
+        pg.submit(i)
+    pg.drain()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    tt = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        parts = [p.numpy().view(np.uint32).reshape(-1, 4) for p in pg.gathered((args.steps - 1) % 2)]
+        unpack_records(np.concatenate(parts), n_total)
+        ranks_seen = sum(int((p[:, 0] != 0xFFFFFFFF).any()) for p in parts)
+        print(json.dumps({
+            "metric": "refined SV loci/sec (whole node)", "value": round(n_total * args.steps / float(tt.item()), 1),
+            "unit": "loci/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(float(tt.item()) / max(args.steps, 1) * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+            "data": "dry run: launcher + shard + gather plumbing on CPU (gloo), no refinement -- not a measurement",
+            "dry_run": True,
+            "config": {"workload": args.workload, "loci_total": n_total, "loci_per_gpu": len(sl),
+                       "parallelism": f"genomic row shard x{world}", "gather": "gloo" if world > 1 else None},
+            "gather_ranks": ranks_seen if world > 1 else 1, "records_verified": True,
+            "cpu_baseline": None,
+            "cpu_baseline_note": "not timed in a dry run",
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one GPU each); without WORLD_SIZE in the environment, N > 1 starts the N "
+                         "rank processes itself; under torch.distributed.run it must equal WORLD_SIZE")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU plumbing check: launcher, shard, gloo gather and the JSON line, no GPU, no refinement")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default=DEFAULT_WORKLOAD)
@@ -170,6 +286,19 @@ def main() -> int:
                     help="diagnostic: scale the workload's locus count (and so its genome) by this factor")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        if args.emulate_shard:
+            ap.error("--emulate-shard runs one rank's slice in one process; it takes no --gpus N > 1")
+        return launch_ranks(args.gpus, sys.argv[1:])
+    world = int(env_world or "1")
+    if world != args.gpus:
+        ap.error(f"WORLD_SIZE={world} from the launcher but --gpus {args.gpus}: they must agree")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -177,10 +306,6 @@ def main() -> int:
     from svtrek_amd import Engine, Params, sim
     from svtrek_amd._lib import RECORD_DTYPE
     from svtrek_amd.distributed import PipelinedGather, padded_rows, shard_workload, unpack_records
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -277,9 +402,11 @@ def main() -> int:
     # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records)
     last = (args.steps - 1) % 2
     verified = None
+    gather_ranks = None
     if rank == 0 and (gather or world == 1) and not args.no_verify and not args.emulate_shard:
-        parts = pg.gathered(last)
-        unpack_records(np.concatenate([p.cpu().numpy().view(np.uint32) for p in parts]), n_total)
+        parts = [p.cpu().numpy().view(np.uint32).reshape(-1, 4) for p in pg.gathered(last)]
+        unpack_records(np.concatenate(parts), n_total)
+        gather_ranks = sum(int((p[:, 0] != 0xFFFFFFFF).any()) for p in parts)
         verified = True
 
     # ---- untimed: the two phases on their own (5 runs each), and a step with the Infinity
@@ -402,8 +529,12 @@ def main() -> int:
                             "note": "value_index_resident: loci/s of the refine launch alone, the index built once "
                                     "(BAI-like amortisation); not the headline"},
             "cpu_baseline": cpu,
+            **({} if cpu is not None else {"cpu_baseline_note":
+                "timed on rank 0 at N = 1 only (a bounded sample of the same workload); this run has N = "
+                f"{world}" if world > 1 else "skipped (--no-cpu-baseline or an emulated shard)"}),
             "work": work,
             "records_verified": verified,
+            "gather_ranks": gather_ranks,
             "setup_s": {"generate": round(gen_s, 2), "shard": round(shard_s, 2), "load_pileup": round(load_s, 2)},
             "pileup_device_bytes": eng.device_bytes,
             "engine_version": _engine_version(),

@@ -343,6 +343,7 @@ typedef struct svt_bam_dec_stats {
     uint64_t rechained;       /* batches whose record starts were re-chained hop by hop        */
     uint64_t inflated_bytes;  /* bytes the batches inflated to                                 */
     double   feed_ms;         /* wall time inside svt_bam_dec_feed (H2D, inflate, decode)       */
+    uint64_t rechained_chunks;/* 64 KiB chunks those re-chains walked (from the first wrong guess) */
 } svt_bam_dec_stats;
 svt_status svt_bam_dec_open(svt_ctx *ctx, int32_t n_targets, svt_bam_dec **out);
 svt_status svt_bam_dec_feed(svt_bam_dec *dec, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,

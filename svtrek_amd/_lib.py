@@ -104,7 +104,7 @@ class SvtLoadStats(C.Structure):
 
 class SvtBamDecStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("records", "reads", "cigar_ops", "cg_restored", "batches", "rechained",
-                                          "inflated_bytes")] + [("feed_ms", C.c_double)]
+                                          "inflated_bytes")] + [("feed_ms", C.c_double), ("rechained_chunks", C.c_uint64)]
 
 
 # every symbol include/svtrek_gpu.h declares

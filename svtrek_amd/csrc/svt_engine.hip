@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.21.1 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.21.2 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -3061,6 +3061,8 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
         return s;
     uint8_t *buf = d->d_buf[d->cur];
     if (n) {
+        // the error word is the context's: order this call after its other streams' calls
+        if ((s = order_on(c, d->st))) return s;
         HIP_TRY(c, hipMemcpyAsync(d->d_comp, comp, comp_bytes, hipMemcpyHostToDevice, d->st));
         HIP_TRY(c, hipMemcpyAsync(d->d_blk, blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->st));
         HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), d->st));
@@ -3071,7 +3073,7 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
     }
     const uint64_t span = N - r0;
     const uint32_t nch = (uint32_t)((span + BD_CHUNK - 1) / BD_CHUNK);
-    BdCheck chk{1u, 0u, 0ull, N, 0u, 0u};
+    BdCheck chk{1u, 0u, 0ull, N, 0u, 0u, 0ull};
     if (nch) {
         if ((s = bd_grow(c, d->d_ch, d->ch_cap, nch)) || (s = bd_grow(c, d->d_base, d->base_cap, nch))) return s;
         hipLaunchKernelGGL(bd_chunk_kernel, dim3(nch), dim3(WAVE), 0, d->st, buf, r0, N, nch, d->n_ref, d->d_ch);
@@ -3086,9 +3088,11 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
             snprintf(m, sizeof m, "%u", ierr);
             return fail(c, SVT_EINVAL, "corrupt BGZF block %s of the batch (does not inflate to its ISIZE)", m);
         }
-        if (!chk.ok) {   // a wrong guess: the exact chain, hop by hop
+        if (!chk.ok) {   // a wrong guess: the exact chain, hop by hop from the first wrong chunk on
             d->stats.rechained++;
-            hipLaunchKernelGGL(bd_chain_kernel, dim3(1), dim3(WAVE), 0, d->st, buf, r0, N, nch, d->d_ch);
+            d->stats.rechained_chunks += nch - chk.kfail;
+            hipLaunchKernelGGL(bd_chain_kernel, dim3(1), dim3(WAVE), 0, d->st, buf, r0, N, nch, chk.kfail, chk.efail,
+                               d->d_ch);
             hipLaunchKernelGGL(bd_check_kernel, dim3(1), dim3(WAVE), 0, d->st, buf, d->d_ch, nch, r0, N, d->d_chk);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipMemcpyAsync(&chk, d->d_chk, sizeof chk, hipMemcpyDeviceToHost, d->st));
@@ -3236,7 +3240,9 @@ svt_status svt_bam_dec_load(svt_bam_dec *d) {
         s = load_core(c, nt, toff.data(), p2.data(), e2.data(), n2.data(), o2.data(), s2.data(), nullptr,
                       d->stats.cigar_ops, pre);
     } else {
-        // the stream stays where the decode wrote it (its spare words zeroed): the context adopts it
+        // the stream stays where the decode wrote it (its spare words zeroed): the context adopts it;
+        // a BAM without records never allocated one, so it gets just the spare words here
+        if ((s = bd_grow(c, d->cols.stream, d->word_cap, d->nwords + STREAM_PAD, d->nwords))) return s;
         HIP_TRY(c, hipMemset(d->cols.stream + d->nwords, 0, STREAM_PAD * 4));
         s = load_core(c, nt, toff.data(), pos.data(), endpos.data(), nc.data(), soff.data(), nullptr, d->cols.stream,
                       d->stats.cigar_ops, pre);

@@ -405,6 +405,7 @@ int audit(int argc, char **argv) {
     std::vector<std::string> gerr(G);
     std::vector<double> load_s(G, 0.0);
     std::vector<size_t> order;
+    svt_bam_dec_stats dst{};
     if (G > 1) {
         order.resize(loci.size());
         std::iota(order.begin(), order.end(), (size_t)0);
@@ -430,6 +431,7 @@ int audit(int argc, char **argv) {
             n = sh.loci.size();
         } else if (ddec.dec) {   // decoded on this device: its pileup, in place
             s = svt_bam_dec_load(ddec.dec);
+            (void)svt_bam_dec_stats_get(ddec.dec, &dst);
             svt_bam_dec_close(ddec.dec);
             ddec.dec = nullptr;
         } else {
@@ -466,7 +468,7 @@ int audit(int argc, char **argv) {
     printf("[INFO] Ended processing variation file\n");
     if (a.verbose)   // --verbose is parsed but unused by the reference; here: stage timings on stderr
         fprintf(stderr, "[svtrek_amd] ingest %.3fs (%s%s)  vcf-read+parse %.3fs (beside the ingest)  "
-                        "load+refine %.3fs (load %.3fs)  print %.3fs  records %zu\n",
+                        "load+refine %.3fs (load %.3fs)  print %.3fs  records %zu%s\n",
                 t_ingest - t0,
                 dev_decode ? "gpu inflate + record decode" : a.gpu_inflate ? "gpu inflate, host parse, kernels " : "cpu",
                 dev_decode ? ("; batch reads " + std::to_string(dstage[0]).substr(0, 5) + "s device feeds " +
@@ -477,7 +479,10 @@ int audit(int argc, char **argv) {
                                    "s inflate calls " + std::to_string(stage[3]).substr(0, 5) + "s parser waits " +
                                    std::to_string(stage[4]).substr(0, 5) + "s").c_str() : "",
                 t_parse_end - t0, t_refine - t_parse, *std::max_element(load_s.begin(), load_s.end()),
-                now_s() - t_refine, loci.size());
+                now_s() - t_refine, loci.size(),
+                dev_decode ? ("  decode: " + std::to_string(dst.batches) + " batches, " + std::to_string(dst.rechained) +
+                              " re-chained (" + std::to_string(dst.rechained_chunks) + " chunks walked hop by hop)").c_str()
+                           : "");
     return 0;
 }
 

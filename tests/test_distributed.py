@@ -227,3 +227,48 @@ def test_gloo_audt_dist_region_shards(tmp_path, world, fail_rank, fail_kind):
     np.testing.assert_array_equal(np.load(tmp_path / "res.npy"), want)
     reads = [int(np.load(tmp_path / f"reads{k}.npy")[0]) for k in range(world)]
     assert max(reads) < r.pileup.n_reads   # each rank read only its region of the BAM
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launcher_spawns_ranks_dry_run(world):
+    """`bench.py --gpus N` (no WORLD_SIZE in the environment) starts N rank processes itself:
+    the gloo dry run shards cfg1, every rank's records reach rank 0 through the gather and
+    exactly one JSON line comes out, with n_gpus = N."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    bench = os.path.join(os.path.dirname(here), "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, bench, "--gpus", str(world), "--dry-run", "--workload", "cfg1_100del_10x",
+                        "--steps", "3", "--warmup", "1"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]   # gloo prints "[Gloo] ..." lines
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["gather_ranks"] == world and out["records_verified"] is True
+    assert out["config"]["loci_total"] == 100 and out["cpu_baseline"] is None
+
+
+def test_bench_refuses_world_size_mismatch():
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    bench = os.path.join(os.path.dirname(here), "bench.py")
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, bench, "--gpus", "4", "--dry-run"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0 and "must agree" in r.stderr
+
+
+def test_bench_launcher_stops_ranks_on_failure():
+    """A rank that fails makes the launcher stop the others and exit non-zero (an unknown
+    workload fails every rank before the first collective)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    bench = os.path.join(os.path.dirname(here), "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, bench, "--gpus", "2", "--dry-run", "--workload", "nope"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and not any(ln.startswith("{") for ln in r.stdout.splitlines())

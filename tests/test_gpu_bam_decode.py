@@ -105,7 +105,40 @@ def test_params_and_empty_file(engine_factory, tmp_path):
     assert st["reads"] == 0 and st["records"] == 3
     got = eng.refine(make_loci([(2, 1, 100000, 101000)]))
     assert int(got["start"][0]) == 0xFFFFFFFF
+    # a header and no record at all: the decode never allocates a stream, load must still work
+    raw0, _ = bamfix.make_bam(seed=14, n_reads=0, unplaced=0)
+    path0 = str(tmp_path / "h.bam")
+    with open(path0, "wb") as f:
+        f.write(bamfix.bgzf_blocks(raw0))
+    eng0 = engine_factory()
+    st0 = host.load_bam_device(eng0, path0)
+    assert st0["reads"] == 0 and st0["records"] == 0
+    got0 = eng0.refine(make_loci([(2, 1, 100000, 101000), (1, 2, 500, 0)]))
+    assert (got0["start"] == 0xFFFFFFFF).all() and (got0["end"] == 0xFFFFFFFF).all()
     path2 = str(tmp_path / "p.bam")
     recs, n_ref = bamfix.write(path2, seed=17)
     _same_as_host(engine_factory, path2, _loci(np.random.default_rng(17), n_ref),
                   params=Params(wider_interval=3000, narrow_interval=100, consensus_min_count=1))
+
+
+def test_wrong_guess_rechains_from_the_failing_chunk(engine_factory, tmp_path):
+    """A record whose aux array holds copies of another record makes the chunks inside it guess
+    a start that is not on the chain: the proof fails there and the batch is re-chained hop by
+    hop from that chunk on, with the host parse's result."""
+    import random
+    import struct
+    raw, recs = bamfix.make_bam(seed=41, n_reads=4000, unplaced=0)
+    hdr_len = len(raw) - sum(len(r["raw"]) for r in recs)
+    rng = random.Random(5)
+    k = len(recs) // 2
+    fake = recs[3]["raw"]
+    payload = fake * (200000 // len(fake) + 1)
+    aux = b"XBBC" + struct.pack("<I", len(payload)) + payload
+    big = bamfix.record(recs[k]["tid"], recs[k]["pos"], b"giant", [(0, 500)], 0, 500, aux, False, rng)
+    body = b"".join(r["raw"] for r in recs[:k]) + big + b"".join(r["raw"] for r in recs[k:])
+    path = str(tmp_path / "g.bam")
+    with open(path, "wb") as f:
+        f.write(bamfix.bgzf_blocks(raw[:hdr_len] + body))
+    st = _same_as_host(engine_factory, path, _loci(np.random.default_rng(41), 3))
+    n_chunks = (len(body) + 65535) // 65536
+    assert st["rechained"] == 1 and 0 < st["rechained_chunks"] < n_chunks
