@@ -261,22 +261,25 @@ uint64_t   svt_poa_deferred(const svt_ctx *ctx);
 /* Bytes of device memory the loaded pileup occupies. */
 uint64_t svt_pileup_device_bytes(const svt_ctx *ctx);
 
-/* Where the last svt_load_pileup spent its time.  The device index (per-read walk ends and
- * slow flags, span-event offsets and lists, the lead arena of refine_end's stop searches)
- * depends only on the pileup, like the BAI the reference's sam_itr_queryi needs
- * (audit.c:271): it is the reference's per-read CIGAR walk (refinement.c:118-159 / :184-221 /
- * :295-318) done once per read instead of once per (window, read). */
+/* Where the last svt_load_pileup spent its time.  The device index (per-read span-event
+ * offsets and the span-event lists) depends only on the pileup, like the BAI the reference's
+ * sam_itr_queryi needs (audit.c:271): it is the reference's per-read CIGAR walk
+ * (refinement.c:118-159 / :184-221 / :295-318) done once per read instead of once per
+ * (window, read). */
 typedef struct svt_load_stats {
     double host_ms;      /* host pass: validation, prefix-max endpos, records, buckets, ranges  */
     double upload_ms;    /* synchronous H2D copies of the caller's arrays (CIGAR words incl.)    */
-    double index_ms;     /* device index build: census, scan of the range totals, emit kernels   */
+    double index_ms;     /* device index build (index_kind's kernels and their scans)            */
     double total_ms;     /* wall time of the whole svt_load_pileup call                          */
-    uint64_t index_bytes;   /* algorithmic bytes one index build moves: the CIGAR stream twice
-                               (4 B/op: census, emit), per read 32 B (census: offsets + record
-                               read, counts written) + 64 B (emit: counts, offsets, record read;
-                               list offsets written), 16 B per span event and lead chunk unit */
+    uint64_t index_bytes;   /* algorithmic bytes one index build moves.  Lane per read (kind 1):
+                               the CIGAR stream twice (4 B/op: census, emit), 80 B per read
+                               (census: offsets + record read, counts written; emit: counts,
+                               offsets, record read, list offsets written), 16 B per span event
+                               written.  Stream walk (kind 2): the stream once, 56 B per read
+                               (offsets, records, staged and placed list offsets), 48 B per span
+                               event (staged, read back, placed) */
     uint64_t span_events;   /* D-list + I-list span events of the pileup                         */
-    uint64_t lead_blocks;   /* 16-B lead chunk units (leading-S reads: header + 4 words / 32 ops) */
+    uint64_t lead_blocks;   /* always 0 (the lead chunks of rounds 1-3 are gone since 0.17)      */
     uint64_t slow_reads;    /* reads whose walk reaches 2^28 bases or position 2^29              */
     uint64_t index_kind;    /* the index build used: 1 lane per read, 2 stream walk              */
 } svt_load_stats;

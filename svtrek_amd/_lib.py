@@ -237,6 +237,8 @@ def load_sim() -> C.CDLL:
     lib.sim_write_bam.restype = C.c_int
     lib.sim_write_bam_region.argtypes = [P, C.c_char_p, C.c_int, C.c_int, C.c_int32, C.c_int64, C.c_int64, C.c_int]
     lib.sim_write_bam_region.restype = C.c_int
+    lib.sim_write_bam_regions.argtypes = [P, C.c_char_p, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int]
+    lib.sim_write_bam_regions.restype = C.c_int
     lib.sim_insseq.argtypes = [P, C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(P),
                                C.POINTER(P)]
     lib.sim_insseq.restype = C.c_int

@@ -834,6 +834,21 @@ int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level
 
 int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, int level, int32_t rtid, int64_t rbeg,
                          int64_t rend, int write_bai) {
+    return sim_write_bam_regions(p, path, with_seq, level, rtid >= 0 ? 1 : 0, &rtid, &rbeg, &rend, write_bai);
+}
+
+/* a record of contig t is written when it overlaps one of the regions of t (all records when
+ * nreg == 0) */
+static int in_regions(int nreg, const int32_t *rt, const int64_t *rb, const int64_t *re, int32_t t, int64_t pos,
+                      int64_t endpos) {
+    if (nreg == 0) return 1;
+    for (int k = 0; k < nreg; k++)
+        if (rt[k] == t && pos < re[k] && endpos > rb[k]) return 1;
+    return 0;
+}
+
+int sim_write_bam_regions(const sim_pileup *p, const char *path, int with_seq, int level, int nreg, const int32_t *rtid,
+                          const int64_t *rbeg, const int64_t *rend, int write_bai) {
     bgzf_w *w = bgzf_open(path, level);
     if (!w) return -1;
     bai_ref *bai = NULL;
@@ -878,9 +893,11 @@ int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, in
     size_t rec_cap = 0;
     static const char nt16[] = "=ACMGRSVTWYHKDBN";
     for (int t = 0; t < p->n_targets; t++) {
-        if (rtid >= 0 && t != rtid) continue;
+        int any = nreg == 0;
+        for (int k = 0; k < nreg; k++) any |= rtid[k] == t;
+        if (!any) continue;
         for (int64_t r = p->tid_off[t]; r < p->tid_off[t + 1]; r++) {
-            if (rtid >= 0 && !(p->pos[r] < rend && p->endpos[r] > rbeg)) continue;
+            if (!in_regions(nreg, rtid, rbeg, rend, t, p->pos[r], p->endpos[r])) continue;
             const uint32_t *ops = p->cigar + p->cig_off[r];
             uint64_t n = p->cig_off[r + 1] - p->cig_off[r];
             int64_t qlen = 0, rlen = 0;

@@ -80,6 +80,10 @@ int sim_write_bam(const sim_pileup *p, const char *path, int with_seq, int level
  * (SAM spec 5.2; empty windows hold the next window's offset).  0 on success. */
 int sim_write_bam_region(const sim_pileup *p, const char *path, int with_seq, int level, int32_t tid, int64_t beg,
                          int64_t end, int write_bai);
+/* the records overlapping any of nreg regions (tid[k], [beg[k], end[k])) -- a shard's halo of
+ * several contigs; nreg == 0: every record */
+int sim_write_bam_regions(const sim_pileup *p, const char *path, int with_seq, int level, int nreg, const int32_t *tid,
+                          const int64_t *beg, const int64_t *end, int write_bai);
 
 #ifdef __cplusplus
 }

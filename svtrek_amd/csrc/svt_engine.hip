@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.21.2 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.22.0 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -1171,10 +1171,7 @@ constexpr uint32_t LV_NONE = 1u << 14;   // no window (INV / other types): NA
 #define LV_WHY(r) 0u
 #endif
 
-#ifndef SVT_PACK
-#define SVT_PACK 1
-#endif
-// Phase 1's packed walk (SVT_PACK): the windows with a span to walk, in wave order, one entry
+// Phase 1's packed walk: the windows with a span to walk, in wave order, one entry
 // each (written by their phase-0 lanes); consecutive windows of <= 64 events together share
 // one 64-event slot.
 struct alignas(16) LvWin {
@@ -1190,9 +1187,7 @@ template <int W>
 struct LaneLds {
     uint16_t stage[W * LV_S];   // parked queries (phase 0 -> 1), band offsets (1 -> 2)
     LvMeta meta[W];
-#if SVT_PACK
     LvWin win[W];
-#endif
 };
 
 // Phase 1 of one window, wave-wide (A4-A7 + the band): the window's span events [E0, E0+len)
@@ -1232,6 +1227,79 @@ __device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, u
 #define SVT_LW_U 4
 #endif
 constexpr int LW_U = SVT_LW_U;   // 64-event slots per step of lane_walk (loads in flight per lane)
+#ifndef SVT_LW_BUF
+#define SVT_LW_BUF 1
+#endif
+// SVT_LW_BUF: lane_walk reads the span through a buffer descriptor of the window's own span
+// (wave-uniform base and byte count, rebuilt per step on the scalar unit): a lane's byte offset
+// is the constant ln * 16 (+ the slot's immediate offset), so a load costs no VALU address
+// arithmetic, and a load past the span returns zeros -- an op-0 (M) event, never a candidate --
+// so no clamp and no partial-slot mask either.  Spans of 2^27 events or more take the
+// wave-wide path (LvQuery), so the byte count fits 32 bits.
+constexpr uint32_t LW_BUF_MAX = 1u << 27;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#ifndef SVT_NB_NA
+#define SVT_NB_NA 1
+#endif
+// SVT_NB_NA: the min_count test (refinement.c:43) on the band size instead of the candidate count.
+// Exact: an accepted cluster lies inside the band (its elements are within ci of an element
+// within range of pos), so the vote returns -1 whenever the band holds fewer than min_count
+// elements, and n < min_count implies nb < min_count.  The walk then keeps no count.
+
+#ifndef SVT_LW_VL
+#define SVT_LW_VL 1
+#endif
+// SVT_LW_VL: one slot of lane_walk as vector arithmetic.  The kernel is bound by scalar issue
+// (one SALU instruction per CU and cycle, against two wave-wide VALU instructions): the mask
+// form (span_cand_mask) combines ~8 compare masks, the band and below / above facts on the
+// scalar unit, ~27 SALU per slot.  Here every test is the sign bit of a difference ("fail"
+// bits), OR-ed per lane; the band is one unsigned compare whose lane mask is the only ballot,
+// and below / above accumulate as sign bits in VGPRs (one ballot each per window).  Exact: the
+// operands' ranges keep every difference inside int32 -- walk positions and candidate values
+// <= 2^30 + 2^28 + 1 (IX_SAT, one op < 2^28), endpos in [1, 2^30) (slow reads carry no events),
+// e < 2^30 (WEXACT), lo >= -2^29 (lane_query), the window start clamped (LwWin).
+#if SVT_LW_VL && !(SVT_LW_BUF && SVT_NB_NA)
+#error "SVT_LW_VL needs SVT_LW_BUF (zero events past the span) and SVT_NB_NA (no candidate count)"
+#endif
+struct LwWin {
+    int32_t b1;     // max(s - 1, -2^30) + 1: the overlap test endpos > s - 1 is endpos - b1 >= 0
+    uint32_t e;
+    int32_t sc;     // s, or 2^31 - 1 when s >= 2^31 (a window start that wrapped: x >= s never holds)
+    int32_t lo1;    // lo + 1: a value v is at or below the band when v - lo1 < 0
+    int32_t hm1;    // hi - 1: at or above it when hm1 - v < 0
+    uint32_t wb;    // hi - lo - 1: in the band when (uint32)(v - lo1) < wb
+};
+__device__ __forceinline__ uint32_t sgn(int32_t d) { return (uint32_t)d >> 31; }
+__device__ __forceinline__ uint32_t opbit(uint32_t set, uint32_t op) { return __builtin_amdgcn_ubfe(set, op, 1); }
+
+// One 64-event slot: the band's lane mask; below / above accumulated into the sign bits of
+// belv / abv; iv = the lane's candidate value.
+template <int KIND>
+__device__ __forceinline__ uint64_t slot_vl(const uint4 &v, const LwWin &W, uint32_t &belv, uint32_t &abv, int32_t &iv) {
+    const uint32_t op = v.y & 0xfu;
+    const uint32_t far = sgn((int32_t)v.z - W.b1) | sgn((int32_t)W.e - (int32_t)v.x);   // no overlap / not reached
+    uint32_t fail;
+    if (KIND == K_INS) {                                                  // refinement.c:299
+        fail = far | (opbit(1u << OP_INS, op) ^ 1u);
+        iv = (int32_t)v.x;
+    } else if (KIND == K_START) {                                         // :124, :147
+        fail = far | (opbit(1u << OP_DEL | 1u << SP_TRAIL, op) ^ 1u) |
+               (opbit(1u << SP_TRAIL, op) & sgn((int32_t)v.x - W.sc));
+        iv = (int32_t)v.x;
+    } else {                                                              // :188, :210-220
+        const uint32_t isD = opbit(1u << OP_DEL, op);
+        const uint32_t lead = opbit(1u << SP_LEAD, op) & (far ^ 1u) & (sgn((int32_t)v.x - W.sc) ^ 1u);
+        const uint32_t brk = lead & sgn((int32_t)W.e - (int32_t)v.w);   // walk passes e: a value >= e + 2
+        abv |= brk << 31;
+        fail = ((isD & (far ^ 1u)) | (lead & (brk ^ 1u))) ^ 1u;
+        iv = (int32_t)(isD ? v.x + (v.y >> 4) + 1u : v.w + 1u);
+    }
+    const uint32_t d = (uint32_t)(iv - W.lo1);
+    const uint32_t pass = (fail ^ 1u) << 31;
+    belv |= d & pass;
+    abv |= (uint32_t)(W.hm1 - iv) & pass;
+    return ballot((d | fail << 31) < W.wb);
+}
 
 template <int KIND>
 __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
@@ -1241,37 +1309,69 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
     const uint4 *ev = (KIND == K_INS ? P.spI : P.spD) + E0;   // wave-uniform base: 32-bit lane offsets
     uint64_t below = 0, above = 0;   // candidates at or below lo / at or above hi
     int32_t n = 0, nb = 0;
+#if SVT_LW_VL
+    uint32_t belv = 0, abv = 0;
+    const LwWin W{max(beg32, -(1 << 30)) + 1, e, (int32_t)min(s, 0x7fffffffu), lo + 1, hi - 1, (uint32_t)(hi - lo - 1)};
+#endif
+#if SVT_LW_BUF
+    const uint64_t evaddr = reinterpret_cast<uint64_t>(ev);
+#endif
     for (uint32_t b = 0; b < len; b += LW_U * WAVE) {
         const uint32_t left = len - b;
         uint4 v[LW_U];
+#if SVT_LW_BUF
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void *>(evaddr + (uint64_t)b * 16u), (short)0, (int)(left * 16u), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < LW_U; u++) {   // all four in flight at once; past the span: zeros
+            const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, ln * 16 + u * WAVE * 16, 0, 0);
+            v[u] = make_uint4(r.x, r.y, r.z, r.w);
+        }
+#else
 #pragma unroll
         for (int u = 0; u < LW_U; u++)   // unconditional (clamped): all four in flight at once
             v[u] = ev[min(b + (uint32_t)(u * WAVE + ln), len - 1u)];
+#endif
 #pragma unroll
         for (int u = 0; u < LW_U; u++) {
             if ((uint32_t)(u * WAVE) >= left) break;
-            const uint32_t rem = left - (uint32_t)(u * WAVE);
+#if SVT_LW_VL
+            int32_t iv;
+            const uint64_t mb = slot_vl<KIND>(v[u], W, belv, abv, iv);
+#else
             uint64_t brk;
             uint64_t cm = span_cand_mask<KIND>(v[u], s, e, beg32, brk);
+#endif
+#if !SVT_LW_BUF
+            const uint32_t rem = left - (uint32_t)(u * WAVE);
             if (rem < (uint32_t)WAVE) {   // the span's last, partial slot: its lanes only
                 const uint64_t in = (1ull << rem) - 1ull;
                 cm &= in;
                 brk &= in;
             }
+#endif
+#if !SVT_LW_VL
             const int32_t iv = (int32_t)(KIND == K_END ? ((v[u].y & 0xfu) == OP_DEL ? v[u].x + (v[u].y >> 4) + 1u
                                                                                    : v[u].w + 1u)
                                                        : v[u].x);
+#if !SVT_NB_NA
             n += (int32_t)__popcll(cm | brk);
+#endif
             above |= brk;
             const uint64_t gt = ballot(iv > lo), lt = ballot(iv < hi);
             below |= cm & ~gt;
             above |= cm & ~lt;
             const uint64_t mb = cm & gt & lt;
+#endif
             // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone)
             if (__builtin_amdgcn_inverse_ballot_w64(mb)) row[min(nb + (int32_t)mbcnt(mb), LV_CAP)] = (uint16_t)(iv - lo);
             nb += (int32_t)__popcll(mb);
         }
     }
+#if SVT_LW_VL
+    below = ballot((int32_t)belv < 0);
+    above = ballot((int32_t)abv < 0);
+#endif
     return LaneBand{n, nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
 }
 
@@ -1313,7 +1413,7 @@ __device__ __forceinline__ void lane_packed(const DevPileup &P, const LvWin *win
         const bool below = (cm & ~gt & rm) != 0ull, above = ((brk | (cm & ~lt)) & rm) != 0ull;
         meta[k].flags = nb > (uint32_t)LV_CAP ? (LV_REDO | LV_WHY(3))
                                               : nb | LV_PENDING | (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u);
-        meta[k].n = (int32_t)__popcll((cm | brk) & rm);
+        meta[k].n = SVT_NB_NA ? 0 : (int32_t)__popcll((cm | brk) & rm);
     }
 }
 
@@ -1458,6 +1558,7 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
         return;
     }
     q.lo = (int32_t)imp - (k.range + max(k.ci, 0));
+    if (q.lo < -(1 << 29)) { q.kind |= LQ_REDO; return; }   // (keeps slot_vl's differences in int32)
     q.len = 0;   // empty span: no reads
     const int tid = L.chrom - 1;
     const int64_t beg = (int64_t)(uint32_t)(q.s - 1u), qend = (int64_t)(uint32_t)(q.e - 1u);
@@ -1481,8 +1582,8 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
     if (lo >= hi) return;
     const uint64_t *off = q.kind == K_INS ? P.spoffI : P.spoffD;
     const uint64_t E0 = off[lo], E1 = off[hi];
-    // spans of 2^31 events or more: the wave-wide path
-    if (E1 - E0 >= 0x80000000ull) { q.kind |= LQ_REDO; return; }
+    // spans of 2^31 events or more (2^27 with the buffer walk): the wave-wide path
+    if (E1 - E0 >= (SVT_LW_BUF ? (uint64_t)LW_BUF_MAX : 0x80000000ull)) { q.kind |= LQ_REDO; return; }
     q.e0[0] = (uint32_t)E0; q.e0[1] = (uint32_t)(E0 >> 32);
     q.len = (uint32_t)(E1 - E0);
 }
@@ -1501,11 +1602,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     const bool band_ok = k.range > SV_MIN_LENGTH / 2 && bw <= LV_WMAX && k.ci >= -LV_WMAX &&
                          SVT_DIAG != 7;
     // ---- phase 0: every window's A2 + A3 at once, one lane each (the dependent loads of
-    // locus -> bucket words -> pos/emax searches -> span bounds run once per LV_W windows),
-    // parked in the window's staging row (read back before that row is written)
-#if SVT_PACK
-    // (packed: the meta row gets its final flags here unless the window has a span to walk,
-    // and the walkable windows' table entries go to win[] in lane order)
+    // locus -> bucket words -> pos/emax searches -> span bounds run once per LV_W windows).
+    // The meta row gets its final flags here unless the window has a span to walk, and the
+    // walkable windows' table entries go to win[] in lane order.
     uint32_t nwin;
     {
         const bool mine = (uint32_t)ln < cnt;
@@ -1535,17 +1634,14 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         nwin = (uint32_t)__popcll(wm);
     }
     wave_sync();
-#else
-    if ((uint32_t)ln < cnt) {
-        LvQuery q{};
-        lane_query(a, g0 + (uint32_t)ln, band_ok, q);
-        *reinterpret_cast<LvQuery *>(L.stage + (uint32_t)ln * LV_S) = q;
-        L.meta[ln].lo = q.lo;     // the window's meta row: what phase 0 knows,
-        L.meta[ln].liw = q.liw;   // phase 1 adds flags and n
+    if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
+        if ((uint32_t)ln < cnt) {
+            const LvMeta mt = L.meta[ln];
+            const LvWin wn = L.win[min((uint32_t)ln, nwin > 0 ? nwin - 1 : 0u)];
+            write_result(a, mt.liw >> 1, mt.liw & 1u, mt.flags ^ (uint32_t)wn.e0 ^ wn.len);
+        }
+        return;
     }
-    wave_sync();
-#endif
-#if SVT_PACK
     // ---- phase 1 (packed): windows of <= 64 events share slots (lane_packed), longer ones are
     // walked alone (lane_walk); their lengths sit in a VGPR, read by the scalar loop
     {
@@ -1585,50 +1681,6 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
-#else
-    if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
-        if ((uint32_t)ln < cnt) {
-            const LvQuery q = *reinterpret_cast<const LvQuery *>(L.stage + (uint32_t)ln * LV_S);
-            write_result(a, q.liw >> 1, q.liw & 1u, (uint32_t)q.kind ^ q.e0[0] ^ q.len);
-        }
-        return;
-    }
-    // ---- phase 1: span walk + band per window (wave-wide).  (Loading the first 64-256 events
-    // of window kw + 1's span before window kw is walked measured 6-9 % slower on cfg4:
-    // profiles/r04_ab2 -- the walk is issue-bound, not latency-bound.)
-    for (uint32_t kw = 0; kw < cnt; kw++) {
-        const LvQuery *qp = reinterpret_cast<const LvQuery *>(L.stage + kw * LV_S);
-        const int32_t qk = uniform_i(qp->kind);
-        const uint32_t s = (uint32_t)uniform_i((int32_t)qp->s), e = (uint32_t)uniform_i((int32_t)qp->e);
-        const int32_t lo = uniform_i(qp->lo);
-        const uint32_t len = (uint32_t)uniform_i((int32_t)qp->len);
-        const uint64_t E0 = (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[0]) |
-                            (uint64_t)(uint32_t)uniform_i((int32_t)qp->e0[1]) << 32;
-        wave_sync();   // the row may be overwritten from here on
-        uint32_t flags = 0;
-        int32_t n = 0;
-        if (qk < 0) {
-            flags = LV_NONE;
-        } else if (qk & LQ_REDO) {
-            flags = LV_REDO | LV_WHY(1);   // a window past WEXACT, per-read stops, the band off
-        } else {
-            LaneBand r{0, 0, 0u};
-            uint16_t *row = L.stage + kw * LV_S;
-            if (len) {
-                if (qk == K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row);
-                else if (qk == K_START) r = lane_walk<K_START>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row);
-                else r = lane_walk<K_END>(a.pile, s, e, E0, len, lo, lo + 2 * bw, row);
-            }
-            flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : (uint32_t)r.nb | LV_PENDING | r.flags;
-            n = r.n;
-        }
-        if (ln == 0) {
-            L.meta[kw].flags = flags;
-            L.meta[kw].n = n;
-        }
-        wave_sync();
-    }
-#endif
     if (SVT_DIAG == 8) {   // diagnostic build: phases 0-1 only (a checksum of their LDS output written out)
         if ((uint32_t)ln < cnt) {
             const LvMeta mt = L.meta[ln];
@@ -1646,7 +1698,8 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0};
         // decisions: no window or fewer than min_count candidates -> NA (refinement.c:43-45);
         // the wave-wide path; or this lane's vote
-        const bool na = mine && ((mt.flags & LV_NONE) || (!(mt.flags & LV_REDO) && mt.n < k.min_count));
+        const bool na = mine && ((mt.flags & LV_NONE) ||
+                                 (!(mt.flags & LV_REDO) && (SVT_NB_NA ? (int32_t)(mt.flags & 0xffu) : mt.n) < k.min_count));
         if (na) write_result(a, mt.liw >> 1, mt.liw & 1u, SVT_NA);
         redo = ballot(mine && !na && (mt.flags & LV_REDO));
         const bool pend = mine && !na && !(mt.flags & LV_REDO) && (mt.flags & LV_PENDING);
@@ -3260,6 +3313,9 @@ void svt_bam_dec_close(svt_bam_dec *d) {
     {
         DevGuard dg(d->c->device);
         if (d->st) (void)hipStreamSynchronize(d->st);
+        // the context's launch order may point at this stream (svt_bam_dec_feed's order_on): all of
+        // its work is done, so nothing later has to wait for it, and it must not be named again
+        if (d->c->have_last && d->c->last_stream == d->st) d->c->have_last = false;
         hfree(d->d_comp); hfree(d->d_blk); hfree(d->d_buf[0]); hfree(d->d_buf[1]);
         hfree(d->d_ch); hfree(d->d_base); hfree(d->d_rec); hfree(d->d_pre); hfree(d->d_chk); hfree(d->d_tmp);
         hfree(d->cols.tid); hfree(d->cols.pos); hfree(d->cols.endpos); hfree(d->cols.nc); hfree(d->cols.soff);

@@ -184,6 +184,22 @@ def write_bam(res: SimResult, path: str, with_seq: bool = False, level: int = 6,
         raise OSError(f"sim_write_bam failed: {path}")
 
 
+def write_bam_regions(res: SimResult, path: str, regions: list[tuple[int, int, int]], with_seq: bool = False,
+                      level: int = 6, bai: bool = True) -> None:
+    """Like write_bam, with the records overlapping any of several (tid, beg, end) regions: one
+    shard's halo over the contigs its loci span (every query of the shard yields the same reads
+    as on the full file)."""
+    if res.handle is None:
+        raise ValueError("generate(..., keep_handle=True) is required to write a BAM")
+    lib = load_sim()
+    tid = np.ascontiguousarray([r[0] for r in regions], dtype=np.int32)
+    beg = np.ascontiguousarray([r[1] for r in regions], dtype=np.int64)
+    end = np.ascontiguousarray([r[2] for r in regions], dtype=np.int64)
+    if lib.sim_write_bam_regions(res.handle.h, path.encode(), 1 if with_seq else 0, level, len(regions),
+                                 tid.ctypes.data, beg.ctypes.data, end.ctypes.data, 1 if bai else 0) != 0:
+        raise OSError(f"sim_write_bam_regions failed: {path}")
+
+
 def write_vcf(loci: np.ndarray, path: str, chrom_prefix: str = "") -> None:
     """Plain `SVTYPE=..;END=..` VCF (the layout BASELINE configs 2-5 use)."""
     names = {1: "INS", 2: "DEL", 3: "INV"}

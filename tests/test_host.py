@@ -3,6 +3,7 @@ against the oracle restatement, the simvcf golden fixtures, and the C-ABI symbol
 import ctypes as C
 import os
 import re
+import sys
 
 import numpy as np
 import oracle_ffi as O
@@ -377,3 +378,23 @@ def test_vcf_reader_long_lines_and_nul(case):
         assert len(want_loci) == 20   # the final line is dropped
     if case in ("final_short_by_one", "grown_buffer"):
         assert len(want_loci) == 21 + (case == "grown_buffer")
+
+
+def test_write_bam_regions_is_a_shard_halo(tmp_path):
+    """sim.write_bam_regions (tools/e2e_shard.py): the records overlapping a shard's per-contig
+    regions refine the shard's loci exactly as the whole pileup does."""
+    import oracle_ffi as O
+    from svtrek_amd import Params, host, sim
+    from svtrek_amd.distributed import shard_rows
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from e2e_shard import shard_regions
+    r = sim.generate(sim.SimConfig(seed=29, n_loci=240, n_targets=4, del_frac=0.5, coverage=8), keep_handle=True)
+    for rank in range(3):
+        loci = r.loci[shard_rows(r.loci, 3, rank)]
+        regions = shard_regions(loci, Params())
+        assert len({t for t, _, _ in regions}) == len(regions) >= 1
+        path = str(tmp_path / f"s{rank}.bam")
+        sim.write_bam_regions(r, path, regions, with_seq=True, level=1)
+        pl, _ = host.read_bam(path, threads=2)
+        assert pl.n_reads < r.pileup.n_reads
+        np.testing.assert_array_equal(O.refine_batch(pl, loci).view(np.uint32), O.refine_batch(r.pileup, loci).view(np.uint32))
