@@ -1503,6 +1503,123 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int3
     return distL < distR ? valL : valR;                                      // :100
 }
 
+#ifndef SVT_VOTE_FLAT
+#define SVT_VOTE_FLAT 0
+#endif
+// lane_vote as flat loops of wave-uniform trip count (SVT_VOTE_FLAT): every step of a pass is
+// one trip -- start the next element (the break test and the cluster bookkeeping of
+// refinement.c:58-64 / :80-86), then either one cluster extension or the evaluation
+// (:65-76 / :87-97) -- with predicated updates instead of divergent branches, so the loops
+// cost no exec-mask bookkeeping on the scalar unit (the kernel's bound).  Same values as
+// lane_vote, element by element.
+// Lane predicates as all-ones / zero VGPR words behind an empty asm (the compiler cannot fold
+// them back into lane masks, whose logic would run on the scalar unit); sel() is one v_bfi.
+__device__ __forceinline__ uint32_t vm(bool c) {
+    uint32_t m = c ? 0xffffffffu : 0u;
+    asm("" : "+v"(m));
+    return m;
+}
+__device__ __forceinline__ int32_t sel(uint32_t m, int32_t a, int32_t b) {
+    return (int32_t)(((uint32_t)a & m) | ((uint32_t)b & ~m));
+}
+__device__ __forceinline__ int32_t lane_vote_flat(const uint16_t *B, int32_t nb, int32_t w, int32_t lo, uint32_t fl,
+                                                  const KParams &k, bool active) {
+    const int32_t ci = k.ci, range = k.range;
+    // elements <= pos + 25 (lower_bound, refinement.c:3-10): a fixed binary search of the <= 32
+    int32_t l0 = 0;
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1) {
+        const int32_t j = l0 + st;
+        const int32_t bj = B[min(j, LV_CAP) - 1];
+        l0 = sel(vm(j <= nb) & vm(bj <= w + SV_MIN_LENGTH / 2), j, l0);
+    }
+    const bool below = fl & LV_BELOW, above = fl & LV_ABOVE;
+    const bool u0 = !below && l0 == 0;                                          // none <= pos+25
+    const bool lt = below || (nb > 0 && (int32_t)B[0] < w - SV_MIN_LENGTH / 2);   // some < pos-25
+    int32_t p = u0 ? 0 : l0 == 0 ? -1 : l0 - 1;
+    if (nb == 0) p = -1;
+    int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
+    int32_t valR = -1, maxR = k.min_count - 1, distR = 0x7fffffff;
+    int32_t res = 0;
+    uint32_t ret = 0;
+    {   // left pass, refinement.c:58: element i from p down, its cluster [kk, i], sum S
+        int32_t i = p, kk = p + 1, a = 0, prev = 0, S = 0;
+        uint32_t act = vm(active && i >= 0), fresh = 0xffffffffu;
+        while (ballot(act != 0u)) {
+            const int32_t bi = B[max(i, 0)];
+            const uint32_t st = act & fresh;
+            const uint32_t brk = st & vm(ref_abs(w - bi) >= range);
+            act &= ~brk;
+            const uint32_t go = st & ~brk;   // element i starts
+            S = sel(go & vm(i < p), S - prev, S);
+            const uint32_t rs = go & vm(kk > i);
+            S = sel(rs, bi, S);
+            kk = sel(rs, i, kk);
+            a = sel(go, bi, a);
+            fresh &= ~go;
+            const int32_t bk = B[max(kk - 1, 0)];
+            const uint32_t ext = act & vm(kk > 0) & vm(bk >= a - ci);          // :61-64
+            kk = sel(ext, kk - 1, kk);
+            S = sel(ext, S + bk, S);
+            const uint32_t ev = act & ~ext;
+            const int32_t c = max(i - kk + 1, 1);
+            const int32_t co = (int32_t)div_small((uint32_t)S + (uint32_t)(c / 2), (uint32_t)c);   // :65
+            const int32_t d = ref_abs(w - co);
+            const uint32_t cnt = ev & vm(c > maxL);                           // :67-76
+            const uint32_t hit = cnt & vm(d < ci);
+            const uint32_t upd = cnt & ~hit & vm(d < distL);
+            ret |= hit;
+            res = sel(hit, lo + co, res);
+            maxL = sel(upd, c, maxL);
+            valL = sel(upd, lo + co, valL);
+            distL = sel(upd, d, distL);
+            prev = sel(ev, a, prev);
+            i = sel(ev, i - 1, i);
+            fresh |= ev;
+            act &= ~hit & ~(ev & vm(i < 0));
+        }
+    }
+    {   // right pass, :80: from the full multiset's upper_bound(pos-25) up, cluster [i, m)
+        const int32_t q = lt ? (!below ? 0 : nb) : (!above ? nb - 1 : nb);
+        int32_t i = q, m = q, a = 0, prev = 0, S = 0;
+        uint32_t act = vm(active && q >= 0 && q < nb) & ~ret, fresh = 0xffffffffu;
+        while (ballot(act != 0u)) {
+            const int32_t bi = B[min(i, LV_CAP)];
+            const uint32_t st = act & fresh;
+            const uint32_t brk = st & vm(ref_abs(w - bi) >= range);
+            act &= ~brk;
+            const uint32_t go = st & ~brk;
+            S = sel(go & vm(i > q), S - prev, S);
+            const uint32_t rs = go & vm(m <= i);
+            S = sel(rs, bi, S);
+            m = sel(rs, i + 1, m);
+            a = sel(go, bi, a);
+            fresh &= ~go;
+            const int32_t bm = B[min(m, LV_CAP)];
+            const uint32_t ext = act & vm(m < nb) & vm(bm <= a + ci);          // :83-86
+            m = sel(ext, m + 1, m);
+            S = sel(ext, S + bm, S);
+            const uint32_t ev = act & ~ext;
+            const int32_t c = max(m - i, 1);
+            const int32_t co = (int32_t)div_small((uint32_t)S + (uint32_t)(c / 2), (uint32_t)c);   // :87
+            const int32_t d = ref_abs(w - co);
+            const uint32_t cnt = ev & vm(c > maxR);                           // :88-97
+            const uint32_t hit = cnt & vm(d < ci);
+            const uint32_t upd = cnt & ~hit & vm(d < distR);
+            ret |= hit;
+            res = sel(hit, lo + co, res);
+            maxR = sel(upd, c, maxR);
+            valR = sel(upd, lo + co, valR);
+            distR = sel(upd, d, distR);
+            prev = sel(ev, a, prev);
+            i = sel(ev, i + 1, i);
+            fresh |= ev;
+            act &= ~hit & ~(ev & vm(i >= nb));
+        }
+    }
+    return ret ? res : distL < distR ? valL : valR;                          // :100
+}
+
 // A2 (audit.c:176-225) for window g: kind (-1: none -> NA), s, e, pos of the vote.
 __device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &li, uint32_t &w, int32_t &chrom,
                                          uint32_t &s, uint32_t &e, uint32_t &imp) {
@@ -1726,8 +1843,15 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             if (pend) {
 #pragma unroll
                 for (int j = 0; j < LV_CAP; j += 2) wrow[j >> 1] = x[j] | x[j + 1] << 16;
+#if SVT_VOTE_FLAT
+            }
+            {
+                const int32_t r = lane_vote_flat(row, nb, bw, mt.lo, mt.flags, k, pend);
+                if (pend) write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
+#else
                 const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k);
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
+#endif
             }
         }
         wave_sync();

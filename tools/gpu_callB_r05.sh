@@ -11,6 +11,9 @@ export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_parity.py tests/test_gpu_workloads.py tests/test_gpu_api.py > "$OUT/pytest.log" 2>&1
 rc=$?; tail -2 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc
+SVTREK_ENGINE_LIB=$PWD/variants/v7_flat.so timeout -k 10 400 python -u -m pytest -x -q --timeout 240 \
+  --timeout-method thread -m gpu tests/test_gpu_parity.py > "$OUT/pytest_flat.log" 2>&1
+rc=$?; tail -2 "$OUT/pytest_flat.log"; [ $rc -eq 0 ] || exit $rc
 NO_TESTS=1 bash tools/gpu_ab_pairs.sh r05_B_ab default\|cfg4_1m_delins_30x_hifi \
   v0_old\|cfg4_1m_delins_30x_hifi \
   v1_buf\|cfg4_1m_delins_30x_hifi \
@@ -18,6 +21,7 @@ NO_TESTS=1 bash tools/gpu_ab_pairs.sh r05_B_ab default\|cfg4_1m_delins_30x_hifi 
   v3_diag6\|cfg4_1m_delins_30x_hifi\|--no-verify \
   v4_diag8\|cfg4_1m_delins_30x_hifi\|--no-verify \
   v6_diag8_novl\|cfg4_1m_delins_30x_hifi\|--no-verify \
+  v7_flat\|cfg4_1m_delins_30x_hifi \
   default\|cfg4_1m_delins_30x_hifi \
   v0_old\|cfg4_1m_delins_30x_hifi \
   v2_novl\|cfg4_1m_delins_30x_hifi || exit $?
