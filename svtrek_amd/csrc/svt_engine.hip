@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.22.0 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.22.1 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -1968,7 +1968,8 @@ struct svt_ctx {
     // device index (svt_index.inc)
     uint64_t *d_part = nullptr;       // [n_ranges + 1]
     uint32_t n_ranges = 0;
-    IxTot *d_agg = nullptr, *d_wbase = nullptr;   // range totals and their exclusive scan (first build: sizing)
+    IxTot *d_agg = nullptr;           // range (group) totals
+    IxTot *d_bsum = nullptr, *d_bpre = nullptr;   // their sums per block of IX_BLK, the blocks' exclusive scan
     uint4 *d_scr = nullptr;                        // stream walk: staged events / offsets per range, overflow flags
     uint2 *d_scrh = nullptr;
     uint32_t *d_ovf = nullptr;
@@ -1977,8 +1978,6 @@ struct svt_ctx {
     int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
                                       // walk (svt_index.inc) -- SVTREK_IX=auto|lane|stream
     uint64_t *d_tot = nullptr;
-    void *d_scan_tmp = nullptr;       // hipcub scan scratch
-    size_t scan_tmp_bytes = 0;
     uint64_t n_evD = 0, n_evI = 0;
     // allele-consensus mode (svt_load_insseq / svt_poa_consensus)
     uint64_t *d_ins_off = nullptr;
@@ -2088,9 +2087,8 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_wbase); hfree(c->d_tot); hfree(c->d_scan_tmp);
+    hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_bsum); hfree(c->d_bpre); hfree(c->d_tot);
     hfree(c->d_scr); hfree(c->d_scrh); hfree(c->d_ovf);
-    c->scan_tmp_bytes = 0;
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
     c->n_evD = c->n_evI = 0;
@@ -2451,7 +2449,8 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.rec = c->d_rec;
     a.part = c->d_part;
     a.agg = c->d_agg;
-    a.wbase = c->d_wbase;
+    a.bsum = c->d_bsum;
+    a.bpre = c->d_bpre;
     a.spoffD = c->d_spoffD;
     a.spoffI = c->d_spoffI;
     a.spD = c->d_spD;
@@ -2483,12 +2482,9 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     else
         hipLaunchKernelGGL(index_kernel, grid1, block1, 0, st, a);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess)   // the ranges' / groups' exclusive prefixes
-        e = hipcub::DeviceScan::ExclusiveScan(c->d_scan_tmp, c->scan_tmp_bytes, c->d_agg, c->d_wbase, IxTotSum(),
-                                              IxTot{}, (int)nparts, st);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(ix_totals_kernel, dim3(1), dim3(64), 0, st, (const IxTot *)c->d_agg,
-                           (const IxTot *)c->d_wbase, nparts, c->d_tot, c->d_spoffD, c->d_spoffI, (uint64_t)c->n_reads);
+    if (e == hipSuccess) {   // the blocks' exclusive prefixes (ix_part_base adds the ranges' within a block)
+        hipLaunchKernelGGL(ix_scan_blocks_kernel, dim3(1), dim3(IX_SCAN_T), 0, st, c->d_bsum, c->d_bpre,
+                           (nparts + IX_BLK - 1) / IX_BLK, c->d_tot, c->d_spoffD, c->d_spoffI, (uint64_t)c->n_reads);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index census: %s", hipGetErrorString(e)));
@@ -2629,16 +2625,11 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
     if ((s = upload<uint2>(c, c->d_cnt, nullptr, 0, std::max<size_t>((size_t)nr, 1)))) return s;
     const size_t NR = std::max<size_t>({(size_t)c->n_ranges, (size_t)c->n_groups, (size_t)1});
     if ((s = upload<IxTot>(c, c->d_agg, nullptr, 0, NR))) return s;
-    if ((s = upload<IxTot>(c, c->d_wbase, nullptr, 0, NR))) return s;
+    const size_t NB = (NR + IX_BLK - 1) / IX_BLK;
+    if ((s = upload<IxTot>(c, c->d_bsum, nullptr, 0, NB))) return s;   // (zeroed: the first build adds into them)
+    if ((s = upload<IxTot>(c, c->d_bpre, nullptr, 0, NB))) return s;
+    HIP_TRY(c, hipMemset(c->d_bsum, 0, NB * sizeof(IxTot)));
     if (c->n_ranges > 0x7fffffffu) return fail(c, SVT_EINVAL, "pileup: %s", "too many index ranges");
-    {
-        size_t need = 0;
-        HIP_TRY(c, hipcub::DeviceScan::ExclusiveScan(nullptr, need, c->d_agg, c->d_wbase, IxTotSum(), IxTot{},
-                                                     (int)NR, (hipStream_t)nullptr));
-        if ((s = upload<unsigned char>(c, reinterpret_cast<unsigned char *&>(c->d_scan_tmp), nullptr, 0,
-                                       std::max<size_t>(need, 1)))) return s;
-        c->scan_tmp_bytes = std::max<size_t>(need, 1);
-    }
     if ((s = upload<uint64_t>(c, c->d_tot, nullptr, 0, IX_NTOT))) return s;
     if (!index_lane(c, nops, (uint64_t)nr)) {   // the stream walk's scratch slots
         const size_t RR = std::max<size_t>(c->n_ranges, 1);
