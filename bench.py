@@ -274,6 +274,8 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch the step's kernels one by one instead of "
+                                                             "replaying them as a HIP graph")
     ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records check")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-sample-loci", type=int, default=1000,
@@ -342,7 +344,10 @@ def main() -> int:
     d_loci = torch.from_numpy(np.ascontiguousarray(sl).view(np.uint8).copy()).to(dev)
     d_index = torch.from_numpy(rows.astype(np.uint32).view(np.int32)).to(dev)
     rec_words = per * RECORD_DTYPE.itemsize // 4
-    stream = torch.cuda.current_stream(dev)
+    # the launch stream: a stream of its own (a HIP graph is captured on it), made current so that
+    # the gather, the events and every torch op of the bench are ordered on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
     gather = world > 1 and not args.no_gather
     pg = PipelinedGather(lambda: torch.full((rec_words,), -1, dtype=torch.int32, device=dev),   # pads: index ~0
@@ -361,6 +366,30 @@ def main() -> int:
     pg.drain()
     eng.sync(sh)
 
+    # The step as HIP graphs (one per gather buffer): the index build's and the refine's launches
+    # (+ the two resets the engine adds to a captured launch, svt_refine_device_records) replayed
+    # as one graph launch -- the whole work every replay, fewer dispatch gaps (an 8-GPU shard's
+    # step is ~0.2 ms of ~10 launches)
+    graphs = []
+    if not args.no_graph:
+        for b in range(2 if gather else 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                step(b)
+            graphs.append(g)
+        for b, g in enumerate(graphs):   # one untimed replay each
+            pg.buffer(b)
+            g.replay()
+        torch.cuda.synchronize(dev)
+        eng.sync(sh)
+
+    def run_step(i: int) -> None:
+        if graphs:
+            pg.buffer(i)   # (waits for the gather that last read this buffer)
+            graphs[i % len(graphs)].replay()
+        else:
+            step(i)
+
     # HIP events on the launch stream: N = 1 -> one pair around the K steps (nothing else runs
     # on that stream; / K = mean step duration incl. dispatch gaps); N > 1 -> a pair per step
     # (gather waits are interleaved on the stream).
@@ -376,7 +405,7 @@ def main() -> int:
     for i in range(args.steps):
         if per_launch:
             ev[i][0].record(stream)
-        step(i)
+        run_step(i)
         if per_launch:
             ev[i][1].record(stream)
         pg.submit(i)
@@ -400,7 +429,7 @@ def main() -> int:
         t_max = float(tt.item())
 
     # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records)
-    last = (args.steps - 1) % 2
+    last = (args.steps - 1) % 2 if (gather or not graphs) else 0   # (one graph without a gather: buffer 0)
     verified = None
     gather_ranks = None
     if rank == 0 and (gather or world == 1) and not args.no_verify and not args.emulate_shard:
@@ -507,6 +536,8 @@ def main() -> int:
                          "step_ms_mean": round(step_ms, 5),
                          "step_ms_timing": "per-step event pairs" if per_launch else
                          "one event pair around the timed steps / K",
+                         "step_launch": "HIP graph replay (index build + refine, captured once)" if graphs
+                         else "kernel launches",
                          "step_ms_cold": round(cold_ms, 5) if cold_ms else None,
                          "phases": {
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),

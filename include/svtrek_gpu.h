@@ -176,7 +176,11 @@ svt_status svt_refine_device(svt_ctx *ctx, const svt_locus *d_loci, size_t n,
                              svt_result *d_out, void *hip_stream);
 
 /* As svt_refine_device, but each result is written as a gather record
- * {d_index[i] (or index_base + i when d_index is NULL), start, end, 0}. */
+ * {d_index[i] (or index_base + i when d_index is NULL), start, end, 0}.
+ * svt_reindex and the svt_refine_device* calls may be captured into a HIP graph (stream
+ * capture on hip_stream, after one uncaptured call on that stream has sized the buffers):
+ * every replay redoes the whole work, with the spill pool and left-over counters reset by the
+ * graph itself.  A replay must not overlap other calls of the context. */
 svt_status svt_refine_device_records(svt_ctx *ctx, const svt_locus *d_loci, size_t n,
                                      const uint32_t *d_index, uint32_t index_base,
                                      svt_record *d_rec, void *hip_stream);

@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.22.1 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.22.2 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -2130,11 +2130,17 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
     if (n > 0x3fffffffull) return fail(c, SVT_EINVAL, "batch too large (%s)", "n > 2^30-1");
     svt_status s = order_on(c, st);
     if (s) return s;
+    // A launch captured into a HIP graph (the caller's stream capture) is replayed with the
+    // epoch and redo-counter parity of its capture, so its graph also clears the pool head and
+    // its redo counter itself (two memset nodes); otherwise nothing per launch is reset.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (st) HIP_TRY(c, hipStreamIsCapturing(st, &cap));
+    const bool captured = cap == hipStreamCaptureStatusActive;
     // no per-launch reset of the spill pool (epoch-tagged head; launches never overlap,
     // order_on); the work counters of a counting launch start from zero; the head word is
     // cleared once per epoch cycle
     c->epoch = c->epoch % ((1u << 24) - 1u) + 1u;
-    if (c->epoch == 1) {   // a new epoch cycle: the pool head starts from zero
+    if (c->epoch == 1 || captured) {   // a new epoch cycle (or every replay): the pool head starts from zero
         HIP_TRY(c, hipMemsetAsync(c->d_ctl, 0, 8, st));
     }
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_ctl + 16, 0, 8 * W_N, st));
@@ -2164,6 +2170,7 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
         a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + c->lane_par;
         a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->lane_par ^ 1u);
         c->lane_par ^= 1u;
+        if (captured) HIP_TRY(c, hipMemsetAsync(a.redo_ctr, 0, sizeof(uint32_t), st));
         // (16 windows a wave for the 250K-window launches of a 125K-locus shard measured slower:
         // 0.132-0.138 vs 0.117-0.121 ms, profiles/r04_sh)
         hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
