@@ -274,8 +274,9 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true")
-    ap.add_argument("--no-graph", action="store_true", help="launch the step's kernels one by one instead of "
-                                                             "replaying them as a HIP graph")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="steps in flight (1 or 2): 2 engine contexts and streams, step i + 1's index build beside "
+                         "step i's refine")
     ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records check")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-sample-loci", type=int, default=1000,
@@ -334,93 +335,73 @@ def main() -> int:
     n_total, n = len(res.loci), len(sl)
     per = padded_rows(n_total, world)
 
-    eng = Engine(params, device=dev.index)
+    # K steps in flight (--inflight K): K engine contexts, each with the pileup and its own index
+    # buffers, and K streams; step i runs on context / stream i % K, so step i + 1's index build
+    # overlaps step i's refine.  Every step is the whole work (index build + refine of all loci).
+    K = max(1, min(2, args.inflight))
+    engs = [Engine(params, device=dev.index) for _ in range(K)]
     t0 = time.perf_counter()
-    eng.load_pileup(spile)
-    load_s = time.perf_counter() - t0
+    for e_ in engs:
+        e_.load_pileup(spile)
+    load_s = (time.perf_counter() - t0) / K
+    eng = engs[0]
     load_stats = eng.load_stats()
     work = eng.count_work(sl)   # exact algorithmic work (counting kernel, untimed)
 
     d_loci = torch.from_numpy(np.ascontiguousarray(sl).view(np.uint8).copy()).to(dev)
     d_index = torch.from_numpy(rows.astype(np.uint32).view(np.int32)).to(dev)
     rec_words = per * RECORD_DTYPE.itemsize // 4
-    # the launch stream: a stream of its own (a HIP graph is captured on it), made current so that
-    # the gather, the events and every torch op of the bench are ordered on it
-    stream = torch.cuda.Stream(dev)
+    # launch streams of their own, the first made current (the gather, the events and every
+    # torch op of the bench are ordered on the stream of the step they belong to)
+    streams = [torch.cuda.Stream(dev) for _ in range(K)]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
     gather = world > 1 and not args.no_gather
     pg = PipelinedGather(lambda: torch.full((rec_words,), -1, dtype=torch.int32, device=dev),   # pads: index ~0
-                         world, rank, enabled=gather)
+                         world, rank, enabled=gather)   # (two buffers: buffer i % 2 <-> context i % K)
 
-    def launch(i: int) -> None:
-        eng.refine_device_records(d_loci.data_ptr(), n, pg.buffer(i).data_ptr(), d_index.data_ptr(), 0, sh)
+    def launch(i: int, k: int = 0) -> None:
+        engs[k].refine_device_records(d_loci.data_ptr(), n, pg.buffer(i).data_ptr(), d_index.data_ptr(), 0,
+                                      streams[k].cuda_stream)
 
-    def step(i: int) -> None:
-        eng.reindex(sh)   # the device index: every read's CIGAR walked once
-        launch(i)         # the batched refine over the rank's loci
-
-    for i in range(args.warmup):
-        step(i)
-        pg.submit(i)
-    pg.drain()
-    eng.sync(sh)
-
-    # The step as HIP graphs (one per gather buffer): the index build's and the refine's launches
-    # (+ the two resets the engine adds to a captured launch, svt_refine_device_records) replayed
-    # as one graph launch -- the whole work every replay, fewer dispatch gaps (an 8-GPU shard's
-    # step is ~0.2 ms of ~10 launches)
-    graphs = []
-    if not args.no_graph:
-        for b in range(2 if gather else 1):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=stream):
-                step(b)
-            graphs.append(g)
-        for b, g in enumerate(graphs):   # one untimed replay each
-            pg.buffer(b)
-            g.replay()
-        torch.cuda.synchronize(dev)
-        eng.sync(sh)
+    def step(i: int, k: int = 0) -> None:
+        engs[k].reindex(streams[k].cuda_stream)   # the device index: every read's CIGAR walked once
+        launch(i, k)                              # the batched refine over the rank's loci
 
     def run_step(i: int) -> None:
-        if graphs:
-            pg.buffer(i)   # (waits for the gather that last read this buffer)
-            graphs[i % len(graphs)].replay()
-        else:
-            step(i)
+        k = i % K
+        with torch.cuda.stream(streams[k]):
+            step(i, k)
+            pg.submit(i)
 
-    # HIP events on the launch stream: N = 1 -> one pair around the K steps (nothing else runs
-    # on that stream; / K = mean step duration incl. dispatch gaps); N > 1 -> a pair per step
-    # (gather waits are interleaved on the stream).
-    per_launch = gather
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps if per_launch else 1)]
+    for i in range(args.warmup):
+        run_step(i)
+    pg.drain()
+    for k, e_ in enumerate(engs):
+        e_.sync(streams[k].cuda_stream)
+
+    # HIP events: the start on stream 0 after a device-wide sync, an end event per step on its
+    # stream; the mean step duration = the last end - the start, / K steps (dispatch gaps and the
+    # overlap of steps in flight included)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    if not per_launch:
-        ev[0][0].record(stream)
+    ev0.record(stream)
     for i in range(args.steps):
-        if per_launch:
-            ev[i][0].record(stream)
         run_step(i)
-        if per_launch:
-            ev[i][1].record(stream)
-        pg.submit(i)
-    if not per_launch:
-        ev[0][1].record(stream)
+        ev[i].record(streams[i % K])
     pg.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    eng.sync(sh)   # raises on a deferred spill-pool overflow
-    if per_launch:
-        step_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-    else:
-        step_ms = ev[0][0].elapsed_time(ev[0][1]) / args.steps
+    for k, e_ in enumerate(engs):
+        e_.sync(streams[k].cuda_stream)   # raises on a deferred spill-pool overflow
+    step_ms = max(ev0.elapsed_time(e_) for e_ in ev) / args.steps
 
     t_max = wall
     if world > 1:
@@ -429,7 +410,7 @@ def main() -> int:
         t_max = float(tt.item())
 
     # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records)
-    last = (args.steps - 1) % 2 if (gather or not graphs) else 0   # (one graph without a gather: buffer 0)
+    last = (args.steps - 1) % 2
     verified = None
     gather_ranks = None
     if rank == 0 and (gather or world == 1) and not args.no_verify and not args.emulate_shard:
@@ -534,10 +515,8 @@ def main() -> int:
                                    (refine_kernel + (", refine_redo_kernel" if refine_kernel == "refine_lane_kernel"
                                                      else "")) + ")",
                          "step_ms_mean": round(step_ms, 5),
-                         "step_ms_timing": "per-step event pairs" if per_launch else
-                         "one event pair around the timed steps / K",
-                         "step_launch": "HIP graph replay (index build + refine, captured once)" if graphs
-                         else "kernel launches",
+                         "step_ms_timing": "HIP events: start on stream 0, the last step's end, / K",
+                         "steps_in_flight": K,
                          "step_ms_cold": round(cold_ms, 5) if cold_ms else None,
                          "phases": {
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
@@ -571,7 +550,8 @@ def main() -> int:
             "engine_version": _engine_version(),
         }
         print(json.dumps(out), flush=True)
-    eng.close()
+    for e_ in engs:
+        e_.close()
     if world > 1:
         dist.destroy_process_group()
     return 0
