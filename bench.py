@@ -274,7 +274,7 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="steps in flight (1 or 2): 2 engine contexts and streams, step i + 1's index build beside "
                          "step i's refine")
     ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records check")
