@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.22.2 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.22.3 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -1434,6 +1434,44 @@ __device__ __forceinline__ void lane_sort(uint32_t (&x)[LV_CAP]) {   // ascendin
             }
 }
 
+#ifndef SVT_LV_OEM
+#define SVT_LV_OEM 1
+#endif
+#ifndef SVT_LV_PREFILL
+#define SVT_LV_PREFILL 1
+#endif
+#ifndef SVT_LV_L0REG
+#define SVT_LV_L0REG 1
+#endif
+// SVT_LV_PREFILL: phase 0 fills every window's band slots with 0xffff, so phase 2 takes its
+// band straight from the row (no per-slot test against the band size).
+// SVT_LV_OEM: Batcher's odd-even merge sort instead of the bitonic network (19 / 63 / 191
+// compare-exchanges for 8 / 16 / 32 elements against 24 / 80 / 240, all ascending).
+__device__ __forceinline__ void lv_cx(uint32_t (&x)[LV_CAP], int i, int j) {
+    const uint32_t p = x[i], q = x[j];
+    x[i] = min(p, q);
+    x[j] = max(p, q);
+}
+template <int LO, int N, int R>
+__device__ __forceinline__ void lv_oe_merge(uint32_t (&x)[LV_CAP]) {
+    if constexpr (2 * R < N) {
+        lv_oe_merge<LO, N, 2 * R>(x);
+        lv_oe_merge<LO + R, N, 2 * R>(x);
+#pragma unroll
+        for (int i = LO + R; i + R < LO + N; i += 2 * R) lv_cx(x, i, i + R);
+    } else {
+        lv_cx(x, LO, LO + R);
+    }
+}
+template <int LO, int N>
+__device__ __forceinline__ void lv_oe_sort(uint32_t (&x)[LV_CAP]) {
+    if constexpr (N > 1) {
+        lv_oe_sort<LO, N / 2>(x);
+        lv_oe_sort<LO + N / 2, N / 2>(x);
+        lv_oe_merge<LO, N, 1>(x);
+    }
+}
+
 // floor(x / c) for x < 2^17, 1 <= c <= 64: ((x + 1/2) * rcp(c)) lies at least 1/(2c) >= 2^-7
 // inside [q, q+1) exactly, and the f32 product is within 2^-9 of it (x + 1/2 < 2^17,
 // v_rcp_f32 within 1 ulp), so the truncation is exact.
@@ -1447,15 +1485,19 @@ __device__ __forceinline__ uint32_t div_small(uint32_t x, uint32_t c) {
 // windows whose ends only move one way along each pass, so their sums are kept up to date
 // element by element (no prefix array).
 __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int32_t w, int32_t lo, uint32_t fl,
-                                             const KParams &k) {
+                                             const KParams &k, int32_t l0 = -1) {
     const int32_t ci = k.ci, range = k.range;
     int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
     int32_t valR = -1, maxR = k.min_count - 1, distR = 0x7fffffff;
     // lower_bound(pos+25) over the band (refinement.c:3-10), started where the full pass would
-    int32_t l0 = 0, h0 = nb;
-    while (l0 < h0) {
-        const int32_t md = (l0 + h0) >> 1;
-        if ((int32_t)B[md] > w + SV_MIN_LENGTH / 2) h0 = md; else l0 = md + 1;
+    // (l0 >= 0: the caller counted the band elements <= pos+25 already)
+    if (l0 < 0) {
+        int32_t h0 = nb;
+        l0 = 0;
+        while (l0 < h0) {
+            const int32_t md = (l0 + h0) >> 1;
+            if ((int32_t)B[md] > w + SV_MIN_LENGTH / 2) h0 = md; else l0 = md + 1;
+        }
     }
     // band_filter's whole-multiset facts: the band's own elements (B[0] its minimum) plus
     // whether candidates lie below / above it
@@ -1729,6 +1771,11 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         if (mine) lane_query(a, g0 + (uint32_t)ln, band_ok, q);
         const bool walk = mine && q.kind >= 0 && !(q.kind & LQ_REDO) && q.len != 0u;
         if (mine) {
+#if SVT_LV_PREFILL
+            uint32_t *row32 = reinterpret_cast<uint32_t *>(L.stage + (uint32_t)ln * LV_S);
+#pragma unroll
+            for (int j = 0; j < LV_CAP / 2; j++) row32[j] = 0xffffffffu;   // unused band slots read as 0xffff
+#endif
             LvMeta m;
             m.lo = q.lo;
             m.liw = q.liw;
@@ -1830,15 +1877,26 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
 #pragma unroll
             for (int j = 0; j < LV_CAP; j += 2) {   // two offsets per 4-byte LDS read
                 const uint32_t v = row32[j >> 1];
+#if SVT_LV_PREFILL
+                x[j] = v & 0xffffu;   // (slots past the band hold 0xffff: phase 0)
+                x[j + 1] = v >> 16;
+#else
                 x[j] = j < nb ? (v & 0xffffu) : 0xffffu;
                 x[j + 1] = j + 1 < nb ? (v >> 16) : 0xffffu;
+#endif
             }
             int32_t nmax = nb;   // wave max of nb: the smallest network that sorts every lane
 #pragma unroll
             for (int d = 32; d > 0; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
+#if SVT_LV_OEM
+            if (nmax <= 8) lv_oe_sort<0, 8>(x);
+            else if (nmax <= 16) lv_oe_sort<0, 16>(x);
+            else lv_oe_sort<0, 32>(x);
+#else
             if (nmax <= 8) lane_sort<8>(x);
             else if (nmax <= 16) lane_sort<16>(x);
             else lane_sort<32>(x);
+#endif
             uint32_t *wrow = reinterpret_cast<uint32_t *>(row);
             if (pend) {
 #pragma unroll
@@ -1849,7 +1907,16 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 const int32_t r = lane_vote_flat(row, nb, bw, mt.lo, mt.flags, k, pend);
                 if (pend) write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
 #else
+#if SVT_LV_L0REG
+                // the band elements <= pos + 25, counted on the sorted registers (no search)
+                int32_t l0 = 0;
+#pragma unroll
+                for (int j = 0; j < LV_CAP; j++) l0 += (int32_t)(x[j] <= (uint32_t)(bw + SV_MIN_LENGTH / 2));
+                l0 = min(l0, nb);
+                const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k, l0);
+#else
                 const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k);
+#endif
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
 #endif
             }
