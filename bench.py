@@ -522,8 +522,8 @@ def main() -> int:
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "lane per read: CIGAR stream twice (4 B/op; census + emit), 80 B/read "
-                                                "(census soff, rec, counts; emit counts, soff, rec, offsets), 16 B/span "
+                             "index_bytes_def": "lane per read: CIGAR stream twice (4 B/op; census + emit), 65 B/read "
+                                                "(census soff, clip byte, counts; emit counts, soff, rec, offsets), 16 B/span "
                                                 "event; stream walk: the stream once, 56 B/read (soff, rec, staged and "
                                                 "placed offsets), 48 B/span event (staged, read back, placed) "
                                                 "(svt_load_stats.index_bytes)",

@@ -276,8 +276,8 @@ typedef struct svt_load_stats {
     double index_ms;     /* device index build (index_kind's kernels and their scans)            */
     double total_ms;     /* wall time of the whole svt_load_pileup call                          */
     uint64_t index_bytes;   /* algorithmic bytes one index build moves.  Lane per read (kind 1):
-                               the CIGAR stream twice (4 B/op: census, emit), 80 B per read
-                               (census: offsets + record read, counts written; emit: counts,
+                               the CIGAR stream twice (4 B/op: census, emit), 65 B per read
+                               (census: offsets + clip byte read, counts written; emit: counts,
                                offsets, record read, list offsets written), 16 B per span event
                                written.  Stream walk (kind 2): the stream once, 56 B per read
                                (offsets, records, staged and placed list offsets), 48 B per span

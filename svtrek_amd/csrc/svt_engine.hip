@@ -2027,6 +2027,7 @@ struct svt_ctx {
     uint64_t n_ops = 0;
     int32_t *d_pos = nullptr, *d_emax = nullptr;
     uint4 *d_rec = nullptr;
+    uint8_t *d_clip8 = nullptr;       // per read its clip bits (rec.z >> 30) alone: the census's 1 B instead of 16
     uint64_t *d_off64 = nullptr;      // stream offsets [n_reads + 1]
     int64_t *d_tid_off = nullptr, *d_bkt_off = nullptr;
     uint2 *d_bkt = nullptr;
@@ -2151,7 +2152,7 @@ svt_status grow_pool(svt_ctx *c) {
 }
 
 void free_pileup(svt_ctx *c) {
-    hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_off64);
+    hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_clip8); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_ins_off); hfree(c->d_ins_bases);
     hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_bsum); hfree(c->d_bpre); hfree(c->d_tot);
@@ -2521,6 +2522,7 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.stream = c->d_cigar;
     a.soff = c->d_off64;
     a.rec = c->d_rec;
+    a.clip8 = c->d_clip8;
     a.part = c->d_part;
     a.agg = c->d_agg;
     a.bsum = c->d_bsum;
@@ -2685,6 +2687,11 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
     if ((s = upload(c, c->d_pos, pos, (size_t)nr))) return s;
     if ((s = upload(c, c->d_emax, emax.data(), (size_t)nr))) return s;
     if ((s = upload(c, c->d_rec, rec.data(), (size_t)nr))) return s;
+    {
+        std::vector<uint8_t> clip8((size_t)std::max<int64_t>(nr, 1), 0);
+        for (int64_t r = 0; r < nr; r++) clip8[(size_t)r] = (uint8_t)(nc[r] >> 30);
+        if ((s = upload(c, c->d_clip8, clip8.data(), clip8.size()))) return s;
+    }
     if ((s = upload(c, c->d_off64, soff, nr > 0 ? (size_t)nr + 1 : 0, nr > 0 ? 0 : 1))) return s;
     if ((s = upload(c, c->d_bkt, bkt.data(), bkt.size()))) return s;
     if ((s = upload(c, c->d_bkt_off, bkt_off.data(), bkt_off.size()))) return s;
@@ -2729,7 +2736,7 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
         // (8 B/read) and events written to scratch, read back, written to their places (16 B/read
         // of offsets, 3 x 16 B/event).
         if (c->load_stats.index_kind == 1)
-            c->load_stats.index_bytes = 8ull * nstream + 80ull * R + 16ull * (c->n_evD + c->n_evI);
+            c->load_stats.index_bytes = 8ull * nstream + 65ull * R + 16ull * (c->n_evD + c->n_evI);
         else
             c->load_stats.index_bytes = 4ull * nstream + 56ull * R + 48ull * (c->n_evD + c->n_evI);
     } else {

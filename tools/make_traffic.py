@@ -37,6 +37,7 @@ STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's
            # index build is either the lane-per-read pair (short reads) or the stream walk (long reads)
     "ix2_census_kernel": "ix2_census_kernel",
     "ix2_emit_kernel": "ix2_emit_kernel",
+    "ix_scan_blocks_kernel": "ix_scan_blocks_kernel",
     "index_kernel": "(anonymous namespace)::index_kernel(",
     "ix_copy_kernel": "ix_copy_kernel",
     "refine_lane_kernel": "refine_lane_kernel",
