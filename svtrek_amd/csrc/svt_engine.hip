@@ -1747,6 +1747,15 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
     q.len = (uint32_t)(E1 - E0);
 }
 
+// SVT_PHASE_PROF (diagnostic builds): every wave of refine_lane_kernel adds its phases' wall
+// time (100 MHz ticks) and work counts into ph_prof, read (and cleared) by svt_diag_phase.
+#ifndef SVT_PHASE_PROF
+#define SVT_PHASE_PROF 0
+#endif
+#if SVT_PHASE_PROF
+__device__ unsigned long long ph_prof[16];
+#define PH_ADD(i, v) atomicAdd(&ph_prof[i], (unsigned long long)(v))
+#endif
 template <int LV_W>
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) {
     __shared__ LaneLds<LV_W> lds_all[WPB];
@@ -1758,6 +1767,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     const KParams &k = a.prm;
     const uint32_t cnt = min((uint32_t)LV_W, nw - g0);
     const int32_t bw = k.range + max(k.ci, 0);   // the band's half-width
+#if SVT_PHASE_PROF
+    const long long pt0 = wall_clock64();
+#endif
     const bool band_ok = k.range > SV_MIN_LENGTH / 2 && bw <= LV_WMAX && k.ci >= -LV_WMAX &&
                          SVT_DIAG != 7;
     // ---- phase 0: every window's A2 + A3 at once, one lane each (the dependent loads of
@@ -1798,6 +1810,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         nwin = (uint32_t)__popcll(wm);
     }
     wave_sync();
+#if SVT_PHASE_PROF
+    const long long pt1 = wall_clock64();
+#endif
     if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
         if ((uint32_t)ln < cnt) {
             const LvMeta mt = L.meta[ln];
@@ -1810,8 +1825,19 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     // walked alone (lane_walk); their lengths sit in a VGPR, read by the scalar loop
     {
         const uint32_t lenv = (uint32_t)ln < nwin ? L.win[ln].len : 0u;
+#if SVT_PHASE_PROF
+        if (ln == 0) PH_ADD(8, nwin);
+        {
+            const uint32_t tl = rdlane(wave_scan_add(lenv), WAVE - 1);
+            if (ln == 0) PH_ADD(9, tl);
+        }
+#endif
         for (uint32_t c = 0; c < nwin;) {
             const uint32_t l0 = rdlane(lenv, (int)c);
+#if SVT_PHASE_PROF
+            if (ln == 0 && l0 > (uint32_t)WAVE) { PH_ADD(10, 1); PH_ADD(11, (l0 + 255u) / 256u); }
+            if (ln == 0 && l0 <= (uint32_t)WAVE) PH_ADD(12, 1);
+#endif
             if (l0 > (uint32_t)WAVE) {
                 const LvWin *wp = &L.win[c];
                 const uint32_t kl = (uint32_t)uniform_i((int32_t)wp->kl);
@@ -1845,6 +1871,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
+#if SVT_PHASE_PROF
+    const long long pt2 = wall_clock64();
+#endif
     if (SVT_DIAG == 8) {   // diagnostic build: phases 0-1 only (a checksum of their LDS output written out)
         if ((uint32_t)ln < cnt) {
             const LvMeta mt = L.meta[ln];
@@ -1888,6 +1917,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             int32_t nmax = nb;   // wave max of nb: the smallest network that sorts every lane
 #pragma unroll
             for (int d = 32; d > 0; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
+#if SVT_PHASE_PROF
+            if (ln == 0) PH_ADD(nmax <= 8 ? 13 : nmax <= 16 ? 14 : 15, 1);
+#endif
 #if SVT_LV_OEM
             if (nmax <= 8) lv_oe_sort<0, 8>(x);
             else if (nmax <= 16) lv_oe_sort<0, 16>(x);
@@ -1923,6 +1955,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
+#if SVT_PHASE_PROF
+    const long long pt3 = wall_clock64();
+#endif
     // ---- the windows voted wave-wide go to refine_redo_kernel (rare: 0.6 % of cfg4's)
     if (SVT_DIAG == 11) {   // diagnostic build: each left-over window's result = 0xF0000000 | its reason
         const bool mine = (uint32_t)ln < cnt;
@@ -1940,6 +1975,12 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         base = rdlane(base, 0);
         if ((redo >> ln) & 1ull) a.redo_list[base + mbcnt(redo)] = g0 + (uint32_t)ln;
     }
+#if SVT_PHASE_PROF
+    if (ln == 0) {
+        const long long pt4 = wall_clock64();
+        PH_ADD(0, pt1 - pt0); PH_ADD(1, pt2 - pt1); PH_ADD(2, pt3 - pt2); PH_ADD(3, pt4 - pt3); PH_ADD(4, 1);
+    }
+#endif
 }
 
 // The lane kernel's left-over windows (band off, > LV_CAP band elements, > CAP candidates,
@@ -2042,6 +2083,8 @@ struct svt_ctx {
     uint2 *d_scrh = nullptr;
     uint32_t *d_ovf = nullptr;
     uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
+    uint64_t *d_ix3 = nullptr;        // single-pass lane build: [2g + q] status words of group g, list q
+    uint32_t ix3_epoch = 0;           // its builds so far (the status words' epoch)
     uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
     int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
                                       // walk (svt_index.inc) -- SVTREK_IX=auto|lane|stream
@@ -2155,7 +2198,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_clip8); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_bsum); hfree(c->d_bpre); hfree(c->d_tot);
+    hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_bsum); hfree(c->d_bpre); hfree(c->d_tot); hfree(c->d_ix3);
     hfree(c->d_scr); hfree(c->d_scrh); hfree(c->d_ovf);
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
@@ -2553,6 +2596,25 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     const dim3 grid2((unsigned)((c->n_groups + IX2_WPB - 1) / IX2_WPB)), block2(64 * IX2_WPB);
     const dim3 grid1((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block1(64 * IX_WPB);
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
+    // one pass when the lists are sized -- except in a stream capture: a graph would replay the
+    // capture's epoch, which the status words of its previous replay already carry
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (lane && !first && SVT_IX2_FUSED && hipStreamIsCapturing(st, &cap) != hipSuccess)
+        return done(fail(c, SVT_EDEVICE, "%s", "hipStreamIsCapturing"));
+    if (lane && !first && SVT_IX2_FUSED && cap == hipStreamCaptureStatusNone) {
+        hipLaunchKernelGGL(ix2_fused_kernel, grid2, block2, 0, st, a2, c->ix3_epoch++, c->d_ix3);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index build: %s", hipGetErrorString(e)));
+        if (ms) {
+            float t0 = 0.f;
+            e = hipEventRecord(ev[1], st);
+            if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
+            if (e == hipSuccess) e = hipEventElapsedTime(&t0, ev[0], ev[1]);
+            if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index timing: %s", hipGetErrorString(e)));
+            *ms = (double)t0;
+        }
+        return done(SVT_OK);
+    }
     if (lane)
         hipLaunchKernelGGL(ix2_census_kernel, grid2, block2, 0, st, a2);
     else
@@ -2712,6 +2774,9 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
     HIP_TRY(c, hipMemset(c->d_bsum, 0, NB * sizeof(IxTot)));
     if (c->n_ranges > 0x7fffffffu) return fail(c, SVT_EINVAL, "pileup: %s", "too many index ranges");
     if ((s = upload<uint64_t>(c, c->d_tot, nullptr, 0, IX_NTOT))) return s;
+    if ((s = upload<uint64_t>(c, c->d_ix3, nullptr, 0, 2 * std::max<size_t>((size_t)c->n_groups, 1)))) return s;
+    HIP_TRY(c, hipMemset(c->d_ix3, 0, 2 * std::max<size_t>((size_t)c->n_groups, 1) * sizeof(uint64_t)));   // no status yet
+    c->ix3_epoch = 0;
     if (!index_lane(c, nops, (uint64_t)nr)) {   // the stream walk's scratch slots
         const size_t RR = std::max<size_t>(c->n_ranges, 1);
         if ((s = upload<uint4>(c, c->d_scr, nullptr, 0, RR * IX_SCAP))) return s;
@@ -2899,7 +2964,9 @@ svt_status svt_sync(svt_ctx *c, void *stream) {
     int32_t status = st2[0];
     if (st2[1]) {   // the index build's guard fired: census and emit disagreed (an engine bug)
         HIP_TRY(c, hipMemset(c->d_ctl + 12, 0, 4));
-        return fail(c, SVT_EDEVICE, "%s", "device index build: emit overran the census's sizes (results invalid)");
+        return fail(c, SVT_EDEVICE, "%s",
+                    st2[1] == 2 ? "device index build: a look-back never ended (results invalid)"
+                                : "device index build: emit overran the census's sizes (results invalid)");
     }
 #if SVT_DIAG == 9
     fprintf(stderr, "[diag] wave-wide (phase 3) windows: %d\n", status >> 8);
@@ -3134,7 +3201,7 @@ svt_status svt_bgzf_inflate_device(svt_ctx *c, const uint8_t *d_comp, const svt_
     // submission order (like every other launch of the context)
     if (svt_status s = order_on(c, st)) return s;
     HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, st, d_comp, d_blocks, (uint32_t)n, d_out, c->d_inferr);
+    hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, st, d_comp, d_blocks, 0u, (uint32_t)n, d_out, c->d_inferr);
     HIP_TRY(c, hipGetLastError());
     return SVT_OK;
 }
@@ -3219,10 +3286,21 @@ void svt_host_free(svt_ctx *c, void *p) {
 // ---- BAM records decoded on the device (svt_bam.inc)
 }  // extern "C"
 
+// SVT_FEED_PARTS: svt_bam_dec_feed copies a batch's compressed bytes in up to this many parts on
+// a copy stream, and inflates part k while part k + 1 crosses PCIe (the batch's blocks are
+// independent); 1 (default): copy, then inflate.  4 parts measured slower end to end on cfg2
+// (3.54 vs 2.12 s, device feeds 3.04 vs 1.70 s, profiles/r05_I).
+#ifndef SVT_FEED_PARTS
+#define SVT_FEED_PARTS 1
+#endif
+constexpr int FEED_PARTS = SVT_FEED_PARTS;
+constexpr size_t FEED_PART_MIN = 256;   // blocks a part at least (each part is one inflate launch)
 struct svt_bam_dec {
     svt_ctx *c = nullptr;
     int32_t n_ref = 0;
     hipStream_t st = nullptr;
+    hipStream_t cst = nullptr;                // the copy stream
+    hipEvent_t pev[FEED_PARTS] = {};          // part k's bytes are on the device
     uint8_t *d_comp = nullptr;
     size_t comp_cap = 0;
     svt_bgzf_block *d_blk = nullptr;
@@ -3272,8 +3350,11 @@ svt_status svt_bam_dec_open(svt_ctx *c, int32_t n_targets, svt_bam_dec **out) {
     if (!d) return fail(c, SVT_ENOMEM, "%s", "host memory");
     d->c = c;
     d->n_ref = n_targets;
-    if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d->d_chk, sizeof(BdCheck)) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&d->d_chk, sizeof(BdCheck)) == hipSuccess;
+    for (auto &e : d->pev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         svt_bam_dec_close(d);
         return fail(c, SVT_EDEVICE, "%s", "BAM decode: stream / buffers");
     }
@@ -3312,13 +3393,26 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
     if (n) {
         // the error word is the context's: order this call after its other streams' calls
         if ((s = order_on(c, d->st))) return s;
-        HIP_TRY(c, hipMemcpyAsync(d->d_comp, comp, comp_bytes, hipMemcpyHostToDevice, d->st));
-        HIP_TRY(c, hipMemcpyAsync(d->d_blk, blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->st));
         HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), d->st));
-        const unsigned grid = (unsigned)std::min<size_t>(n, (size_t)INF_GRID);
-        hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, d->st, d->d_comp, d->d_blk, (uint32_t)n, buf + T,
-                           c->d_inferr);
-        HIP_TRY(c, hipGetLastError());
+        // the parts: consecutive blocks, each part's bytes the span its blocks cover (the previous
+        // call's inflates are done: it synchronised d->st before returning)
+        const size_t np = std::max<size_t>(1, std::min<size_t>((size_t)FEED_PARTS, n / FEED_PART_MIN));
+        HIP_TRY(c, hipMemcpyAsync(d->d_blk, blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->cst));
+        for (size_t p = 0; p < np; p++) {
+            const size_t b0 = n * p / np, b1 = n * (p + 1) / np;
+            uint64_t lo = ~0ull, hi = 0;
+            for (size_t i = b0; i < b1; i++) {
+                lo = std::min<uint64_t>(lo, blocks[i].coff);
+                hi = std::max<uint64_t>(hi, blocks[i].coff + blocks[i].clen);
+            }
+            if (hi > lo) HIP_TRY(c, hipMemcpyAsync(d->d_comp + lo, comp + lo, hi - lo, hipMemcpyHostToDevice, d->cst));
+            HIP_TRY(c, hipEventRecord(d->pev[p], d->cst));
+            HIP_TRY(c, hipStreamWaitEvent(d->st, d->pev[p], 0));
+            const unsigned grid = (unsigned)std::min<size_t>(b1 - b0, (size_t)INF_GRID);
+            hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, d->st, d->d_comp, d->d_blk, (uint32_t)b0,
+                               (uint32_t)(b1 - b0), buf + T, c->d_inferr);
+            HIP_TRY(c, hipGetLastError());
+        }
     }
     const uint64_t span = N - r0;
     const uint32_t nch = (uint32_t)((span + BD_CHUNK - 1) / BD_CHUNK);
@@ -3412,6 +3506,15 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
     d->stats.feed_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     return SVT_OK;
 }
+
+#if SVT_PHASE_PROF
+// diagnostic builds: refine_lane_kernel's phase times and counts since the last call (then cleared)
+int svt_diag_phase(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ph_prof), sizeof ph_prof) != hipSuccess) return 1;
+    const unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ph_prof), z, sizeof z) != hipSuccess;
+}
+#endif
 
 svt_status svt_bam_dec_stats_get(const svt_bam_dec *d, svt_bam_dec_stats *out) {
     if (!d || !out) return SVT_EINVAL;
@@ -3516,7 +3619,11 @@ void svt_bam_dec_close(svt_bam_dec *d) {
         hfree(d->d_ch); hfree(d->d_base); hfree(d->d_rec); hfree(d->d_pre); hfree(d->d_chk); hfree(d->d_tmp);
         hfree(d->cols.tid); hfree(d->cols.pos); hfree(d->cols.endpos); hfree(d->cols.nc); hfree(d->cols.soff);
         hfree(d->cols.stream);
+        if (d->cst) (void)hipStreamSynchronize(d->cst);
+        for (auto &e : d->pev)
+            if (e) (void)hipEventDestroy(e);
         if (d->st) (void)hipStreamDestroy(d->st);
+        if (d->cst) (void)hipStreamDestroy(d->cst);
     }
     delete d;
 }

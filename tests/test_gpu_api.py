@@ -158,5 +158,36 @@ def test_reindex_keeps_results(engine_factory):
     _same(eng.refine(r.loci), want)
 
 
+def test_graph_replay_reindex(engine_factory):
+    """svt_reindex + svt_refine_device captured into a HIP graph (torch.cuda.graph) replay with
+    the oracle's results every time: the capture takes the two-pass index build (a replayed
+    single-pass build would carry its capture's epoch) and the refine resets its own counters."""
+    r = _workload(n_loci=3000, seed=71)
+    eng = engine_factory()
+    eng.load_pileup(r.pileup)
+    want = O.refine_batch(r.pileup, r.loci, threads=8)
+    n = len(r.loci)
+    d_loci = torch.from_numpy(r.loci.view(np.uint8).copy()).cuda()
+    d_out = torch.zeros(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):   # warm-up: a single-pass rebuild outside the capture
+        eng.reindex(s.cuda_stream)
+        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    _same(d_out.cpu().numpy().view(RESULT_DTYPE), want)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        eng.reindex(s.cuda_stream)
+        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), s.cuda_stream)
+    for _ in range(3):
+        d_out.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        _same(d_out.cpu().numpy().view(RESULT_DTYPE), want)
+    eng.reindex()   # and single-pass rebuilds after the replays
+    _same(eng.refine(r.loci), want)
+
+
 def test_locus_dtype_layout():
     assert LOCUS_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 16
