@@ -1375,6 +1375,121 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
     return LaneBand{n, nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
 }
 
+#ifndef SVT_LV_STREAM
+#define SVT_LV_STREAM 0
+#endif
+#ifndef SVT_LV_SMAX
+#define SVT_LV_SMAX 512
+#endif
+// SVT_LV_STREAM: the windows of WAVE < len <= LV_SMAX span events (cfg4: ~93 % of the walked
+// windows, ~130 events each) are walked as ONE stream of 64-event slots -- each window's span in
+// ceil(len / 64) slots, the windows one after another -- with LV_SQ slots in flight across
+// window boundaries.  lane_walk issues a window's loads, waits for them and only then goes on
+// to the next window: one memory round trip per window, and a wave walks ~24 of them (phase
+// attribution, profiles/r05_I: the walk is 86 % of a wave's time).  Here the loads of the next
+// windows' slots are already in flight while a window's last slots are tested.  The issue side
+// and the test side each keep a cursor (window, slot) over the same sequence; a slot past the
+// stream's end is a load through a zero-size buffer descriptor (zeros, no memory access), so
+// every step issues exactly one load and the waits stay fixed.
+// Off by default: correct, but slower -- cfg4 refine 0.724-0.735 vs 0.617-0.619 ms, rank 3 of 8
+// 0.133 vs 0.106 ms (profiles/r05_K); the walk's per-wave time did not drop (phase attribution
+// unchanged), so the per-window round trip was not what held it, and the two cursors' scalar
+// work is extra issue on a kernel bound by it.
+constexpr uint32_t LV_SMAX = SVT_LV_SMAX;
+static_assert(LV_SMAX > WAVE && LV_SMAX % WAVE == 0, "LV_SMAX: whole slots, more than one");
+template <int W>
+__device__ __forceinline__ void lane_stream(const DevPileup &P, LaneLds<W> &L, uint64_t mid, uint32_t total, int32_t bw) {
+    const int ln = lane_id();
+    // issue cursor: windows not yet opened, the open window's next slot / slot count, its span
+    uint64_t mi = mid;
+    uint32_t is = 0, ins = 0, ilen = 0;
+    uint64_t ibase = reinterpret_cast<uint64_t>(P.spD);
+    auto issue = [&](uint4 &dst) {
+        if (is == ins) {
+            if (mi) {
+                const uint32_t c = (uint32_t)__builtin_ctzll(mi);
+                mi &= mi - 1ull;
+                const LvWin *wp = &L.win[c];
+                const uint32_t kind = (uint32_t)uniform_i((int32_t)wp->kl) & 0xffu;
+                const uint64_t e0 = (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)wp->e0) |
+                                    (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)(wp->e0 >> 32)) << 32;
+                ilen = (uint32_t)uniform_i((int32_t)wp->len);
+                ibase = reinterpret_cast<uint64_t>((kind == (uint32_t)K_INS ? P.spI : P.spD) + e0);
+                ins = (ilen + (uint32_t)WAVE - 1u) / (uint32_t)WAVE;
+            } else {
+                ilen = 0;
+                ins = 0;
+            }
+            is = 0;
+        }
+        const uint32_t at = is * (uint32_t)WAVE;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void *>(ibase + (uint64_t)at * 16u), (short)0, (int)(ilen > at ? (ilen - at) * 16u : 0u), 0x00020000);
+        const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, ln * 16, 0, 0);
+        dst = make_uint4(r.x, r.y, r.z, r.w);
+        is++;
+    };
+    // test cursor: the same sequence
+    uint64_t mp = mid;
+    uint32_t ps = 0, pns = 0, pkind = 0, pkw = 0;
+    int32_t plo = 0, nb = 0;
+    uint32_t belv = 0, abv = 0;
+    LwWin Wn{0, 0, 0, 0, 0, 0};
+    auto test = [&](const uint4 &v) {
+        if (ps == pns) {   // the next window opens
+            if (!mp) return;   // (the last step's slots past the stream's end)
+            const uint32_t c = (uint32_t)__builtin_ctzll(mp);
+            mp &= mp - 1ull;
+            const LvWin *wp = &L.win[c];
+            const uint32_t kl = (uint32_t)uniform_i((int32_t)wp->kl);
+            const uint32_t s = (uint32_t)uniform_i((int32_t)wp->s), e = (uint32_t)uniform_i((int32_t)wp->e);
+            const uint32_t len = (uint32_t)uniform_i((int32_t)wp->len);
+            plo = uniform_i(wp->lo);
+            pkind = kl & 0xffu;
+            pkw = kl >> 8;
+            const int32_t beg32 = (int32_t)(uint32_t)(s - 1u), hi = plo + 2 * bw;
+            Wn = LwWin{max(beg32, -(1 << 30)) + 1, e, (int32_t)min(s, 0x7fffffffu), plo + 1, hi - 1, (uint32_t)(hi - plo - 1)};
+            pns = (len + (uint32_t)WAVE - 1u) / (uint32_t)WAVE;
+            ps = 0;
+            nb = 0;
+            belv = 0;
+            abv = 0;
+        }
+        int32_t iv;
+        uint64_t mb;
+        if (pkind == (uint32_t)K_INS) mb = slot_vl<K_INS>(v, Wn, belv, abv, iv);
+        else if (pkind == (uint32_t)K_START) mb = slot_vl<K_START>(v, Wn, belv, abv, iv);
+        else mb = slot_vl<K_END>(v, Wn, belv, abv, iv);
+        uint16_t *row = L.stage + pkw * LV_S;
+        // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone)
+        if (__builtin_amdgcn_inverse_ballot_w64(mb)) row[min(nb + (int32_t)mbcnt(mb), LV_CAP)] = (uint16_t)(iv - plo);
+        nb += (int32_t)__popcll(mb);
+        if (++ps == pns) {   // the window's last slot: its meta row (as lane_walk's caller writes it)
+            const bool below = ballot((int32_t)belv < 0) != 0ull, above = ballot((int32_t)abv < 0) != 0ull;
+            if (ln == 0) {
+                L.meta[pkw].flags = nb > LV_CAP ? LV_REDO | LV_WHY(3)
+                                                : (uint32_t)nb | LV_PENDING | (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u);
+                L.meta[pkw].n = 0;
+            }
+        }
+    };
+    uint4 r0, r1, r2, r3;   // LV_SQ = 4 slots in flight, a static ring
+    issue(r0);
+    issue(r1);
+    issue(r2);
+    issue(r3);
+    for (uint32_t u = 0; u < total; u += 4) {   // (no early exits: the waits stay static)
+        test(r0);
+        issue(r0);
+        test(r1);
+        issue(r1);
+        test(r2);
+        issue(r2);
+        test(r3);
+        issue(r3);
+    }
+}
+
 // One 64-event slot holding the whole spans of consecutive walkable windows win[c0..]: bit i of
 // M marks the first lane of a window (bit 0 always), tot <= 64 events in all.  Lane j walks
 // event j - f of the window that starts at f = the highest mark <= j, with that window's own
@@ -1839,6 +1954,12 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             if (ln == 0 && l0 <= (uint32_t)WAVE) PH_ADD(12, 1);
 #endif
             if (l0 > (uint32_t)WAVE) {
+#if SVT_LV_STREAM
+                if (l0 <= LV_SMAX) {   // lane_stream's
+                    c++;
+                    continue;
+                }
+#endif
                 const LvWin *wp = &L.win[c];
                 const uint32_t kl = (uint32_t)uniform_i((int32_t)wp->kl);
                 const uint32_t s = (uint32_t)uniform_i((int32_t)wp->s), e = (uint32_t)uniform_i((int32_t)wp->e);
@@ -1869,6 +1990,16 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             lane_packed(a.pile, L.win, L.meta, L.stage, c, M, tot, 2 * bw);
             c = c1;
         }
+#if SVT_LV_STREAM
+        {
+            const bool md = (uint32_t)ln < nwin && lenv > (uint32_t)WAVE && lenv <= LV_SMAX;
+            const uint64_t mid = ballot(md);
+            if (mid) {
+                const uint32_t total = rdlane(wave_scan_add(md ? (lenv + (uint32_t)WAVE - 1u) / (uint32_t)WAVE : 0u), WAVE - 1);
+                lane_stream<LV_W>(a.pile, L, mid, total, bw);
+            }
+        }
+#endif
         wave_sync();
     }
 #if SVT_PHASE_PROF
@@ -2056,7 +2187,8 @@ struct svt_ctx {
     svt_params prm{};
     int device = 0;
     bool lane_vote = true;        // refine_lane_kernel from 64K windows up; SVTREK_GATHER=span1: refine_span_kernel always
-    uint64_t ix_ranges = 131072;  // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each
+    uint64_t ix_ranges = 32768;   // index ranges per pileup (SVTREK_IX_RANGES, A/B): ~n_ops / this ops each,
+                                  // at most IX_TMAX ops (and IX_RCAP reads) a range
     int lane_w = 0;               // SVTREK_LANE_W=32 forces the lane kernel at every batch size (tests)
     uint32_t *d_redo = nullptr;   // lane-vote launches: left-over window list
     size_t redo_cap = 0;
@@ -2722,7 +2854,11 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
     std::vector<uint2> bkt((size_t)bkt_off[(size_t)nt]);
     parallel_for((size_t)nt, 16, [&](size_t t) { std::copy(bk[t].begin(), bk[t].end(), bkt.begin() + bkt_off[t]); });
     // ---- ranges of the index build: ~T stream ops each, cut at read starts and contig starts
-    const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / c->ix_ranges, 2048), 1ull << 26);
+    // 32 768 ranges, of at most 65 536 ops: cfg2 index 0.602 -> 0.531 ms, cfg3 2.30 -> 2.19 ms
+    // against 131 072 ranges (profiles/r05_J; fewer, longer ranges cross fewer range-boundary
+    // slots), while cfg5's 9 G ops keep ~137 K ranges (the stage's 96 events a range).
+    constexpr uint64_t IX_TMAX = 65536;
+    const uint64_t T = std::min<uint64_t>(std::max<uint64_t>(nstream / c->ix_ranges, 2048), IX_TMAX);
     std::vector<std::vector<uint64_t>> pt((size_t)nt);
     parallel_for((size_t)nt, 16, [&](size_t t) {
         for (int64_t r = tid_off[t], r1 = tid_off[t + 1]; r < r1;) {

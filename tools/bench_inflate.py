@@ -25,6 +25,7 @@ def main() -> int:
     ap.add_argument("--scale", type=float, default=0.1)
     ap.add_argument("-t", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--phase", action="store_true", help="read a -DSVT_PHASE_PROF=1 build's counters")
     ap.add_argument("--level", type=int, default=1)
     a = ap.parse_args()
     from dataclasses import replace
@@ -44,14 +45,25 @@ def main() -> int:
     comp = np.fromfile(path, dtype=np.uint8)
     blocks = block_table(comp)
     out_bytes = int(blocks["uoff"][-1]) + int(blocks["ulen"][-1])
+    prof = None
     with Engine(Params(), device=0) as eng:
         eng.bgzf_inflate(comp, blocks, out_bytes)   # warm-up (buffers, code object)
+        if a.phase:   # a -DSVT_PHASE_PROF=1 build (SVTREK_ENGINE_LIB): clear, then read after the reps
+            import ctypes as C
+            buf = (C.c_ulonglong * 16)()
+            eng.lib.svt_diag_phase(buf)
         kms, api = [], []
         for _ in range(a.reps):
             t = time.perf_counter()
             out = eng.bgzf_inflate(comp, blocks, out_bytes)
             api.append(time.perf_counter() - t)
             kms.append(eng.last_inflate_ms())
+        if a.phase:
+            eng.lib.svt_diag_phase(buf)
+            v = [int(x) / a.reps for x in buf]
+            names = ["hdr_ticks", "codes_ticks", "deflate_blocks", "dynamic", "stored_bytes", "literals", "matches",
+                     "match_bytes", "far_matches", "bgzf_blocks", "bgzf_ticks"]
+            prof = dict(zip(names, v))
     # host: zlib per block on T threads (zlib releases the GIL)
     cb = comp.tobytes()
 
@@ -72,7 +84,7 @@ def main() -> int:
         "kernel_ms": round(k, 3), "kernel_gbs": round(out_bytes / (k * 1e-3) / 1e9, 2),
         "api_s": round(min(api), 4), "api_gbs": round(out_bytes / min(api) / 1e9, 2),
         "host_zlib_threads": T, "host_s": round(host_s, 3), "host_gbs": round(out_bytes / host_s / 1e9, 3),
-        "identical_to_zlib": ok, "prep_s": round(prep, 1)}))
+        "identical_to_zlib": ok, "prep_s": round(prep, 1), **({"phase": prof} if prof else {})}))
     return 0 if ok else 1
 
 
