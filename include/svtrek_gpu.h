@@ -335,7 +335,11 @@ void  svt_host_free(svt_ctx *ctx, void *p);
  *   svt_bam_dec_feed:  the next batch of whole BGZF blocks of the file, in order (host buffers,
  *                      the layout of svt_bgzf_inflate, uoff relative to the batch); the first
  *                      `skip` inflated bytes of the first batch are the BAM header (not records);
- *                      a record may span batches.  Synchronous.
+ *                      a record may span batches.  Pipelined one batch deep: the call returns
+ *                      once its batch's bytes are on the device and its inflate is launched, and
+ *                      that batch is decoded by the next call or by svt_bam_dec_load (so a
+ *                      corrupt block or record may be reported there); the host buffers may be
+ *                      reused as soon as the call returns.
  *   svt_bam_dec_load:  at the end of the file: the decoded pileup becomes ctx's pileup, exactly
  *                      as svt_load_pileup of the same reads (a file not sorted by coordinate is
  *                      sorted, as the host ingest does); SVT_EINVAL for a truncated last record.

@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.22.3 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.23.0 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -1188,79 +1188,43 @@ struct LaneLds {
     uint16_t stage[W * LV_S];   // parked queries (phase 0 -> 1), band offsets (1 -> 2)
     LvMeta meta[W];
     LvWin win[W];
+    uint32_t sink[WAVE];        // lane_walk: the store target of lanes without a band member
 };
 
 // Phase 1 of one window, wave-wide (A4-A7 + the band): the window's span events [E0, E0+len)
-// are tested 64 * LW_U at a time (LW_U 16-B loads per lane in flight; lane offsets relative to the
-// span, clamped, masked), and each candidate goes straight to the exact band of consensus_pos
-// (band_filter's rule, see there): members in (lo, hi) are written to the window's row as
-// 16-bit offsets from lo, and whether any candidate lies at or below lo / at or above hi is
-// an OR-ed lane mask (with the band they give the whole-multiset facts, lane_vote).  Values are
-// walk positions < 2^29 + 1 (reads reaching 2^28 bases or position 2^29 are slow and carry
-// no events), so every candidate is >= 0 and within +-2^30: no int64 path is ever needed.
-// refine_end's leading-S reads whose walk passes e count as one candidate at or above the
-// band's high end (KParams::sent_ok).
+// are tested 64 * LW_U at a time (LW_U 16-B loads per lane in flight), and each candidate goes
+// straight to the exact band of consensus_pos (band_filter's rule, see there): members in
+// (lo, hi) are written to the window's row as 16-bit offsets from lo, and whether any candidate
+// lies at or below lo / at or above hi is accumulated per lane (with the band they give the
+// whole-multiset facts, lane_vote).  Values are walk positions < 2^29 + 1 (reads reaching 2^28
+// bases or position 2^29 are slow and carry no events), so every candidate is >= 0 and within
+// +-2^30: no int64 path is ever needed.  refine_end's leading-S reads whose walk passes e count
+// as one candidate at or above the band's high end (KParams::sent_ok).
 struct LaneBand {
-    int32_t n;        // candidates collected (before the stop searches)
     int32_t nb;       // band members (> LV_CAP: the row overflowed)
     uint32_t flags;   // LV_BELOW | LV_ABOVE
 };
 
-// span_cand as lane masks, one compare per ballot (each folds into one v_cmp writing an SGPR
-// pair; the conditions are combined on the scalar unit).  refine_end's value is x + len + 1
-// for a D op and walk end + 1 for a leading S that does not break; brk: a leading S whose walk
-// passes e (a candidate at e + 2 >= the band's high end).
-template <int KIND>
-__device__ __forceinline__ uint64_t span_cand_mask(const uint4 &v, uint32_t s, uint32_t e, int32_t beg32,
-                                                   uint64_t &brk) {
-    const uint32_t x = v.x, op = v.y & 0xfu;
-    const uint64_t ovl = ballot((int32_t)v.z > beg32), le = ballot(x <= e);
-    brk = 0;
-    if (KIND == K_INS) return ovl & le & ballot(op == OP_INS);                                  // refinement.c:299
-    if (KIND == K_START) return ovl & le & (ballot(op == OP_DEL) | (ballot(op == SP_TRAIL) & ballot(s <= x)));
-    const uint64_t lead = ovl & le & ballot(op == SP_LEAD) & ballot(s <= x);                    // :210-220
-    brk = lead & ballot(v.w > e);
-    return (ovl & le & ballot(op == OP_DEL)) | (lead & ~brk);                                   // :188-199
-}
-
-#ifndef SVT_LW_U
-#define SVT_LW_U 4
-#endif
-constexpr int LW_U = SVT_LW_U;   // 64-event slots per step of lane_walk (loads in flight per lane)
-#ifndef SVT_LW_BUF
-#define SVT_LW_BUF 1
-#endif
-// SVT_LW_BUF: lane_walk reads the span through a buffer descriptor of the window's own span
-// (wave-uniform base and byte count, rebuilt per step on the scalar unit): a lane's byte offset
-// is the constant ln * 16 (+ the slot's immediate offset), so a load costs no VALU address
-// arithmetic, and a load past the span returns zeros -- an op-0 (M) event, never a candidate --
-// so no clamp and no partial-slot mask either.  Spans of 2^27 events or more take the
-// wave-wide path (LvQuery), so the byte count fits 32 bits.
+constexpr int LW_U = 4;   // 64-event slots per step of lane_walk (loads in flight per lane)
+// lane_walk reads the span through a buffer descriptor of the window's own span (wave-uniform
+// base and byte count): a lane's byte offset is the constant ln * 16 (+ the slot's immediate
+// offset), so a load costs no VALU address arithmetic, and a load past the span returns zeros --
+// an op-0 (M) event, never a candidate -- so no clamp and no partial-slot mask either.  Spans of
+// 2^27 events or more take the wave-wide path (LvQuery), so the byte count fits 32 bits.
 constexpr uint32_t LW_BUF_MAX = 1u << 27;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#ifndef SVT_NB_NA
-#define SVT_NB_NA 1
-#endif
-// SVT_NB_NA: the min_count test (refinement.c:43) on the band size instead of the candidate count.
+// The min_count test (refinement.c:43) is made on the band size instead of the candidate count.
 // Exact: an accepted cluster lies inside the band (its elements are within ci of an element
 // within range of pos), so the vote returns -1 whenever the band holds fewer than min_count
 // elements, and n < min_count implies nb < min_count.  The walk then keeps no count.
 
-#ifndef SVT_LW_VL
-#define SVT_LW_VL 1
-#endif
-// SVT_LW_VL: one slot of lane_walk as vector arithmetic.  The kernel is bound by scalar issue
-// (one SALU instruction per CU and cycle, against two wave-wide VALU instructions): the mask
-// form (span_cand_mask) combines ~8 compare masks, the band and below / above facts on the
-// scalar unit, ~27 SALU per slot.  Here every test is the sign bit of a difference ("fail"
-// bits), OR-ed per lane; the band is one unsigned compare whose lane mask is the only ballot,
-// and below / above accumulate as sign bits in VGPRs (one ballot each per window).  Exact: the
-// operands' ranges keep every difference inside int32 -- walk positions and candidate values
-// <= 2^30 + 2^28 + 1 (IX_SAT, one op < 2^28), endpos in [1, 2^30) (slow reads carry no events),
-// e < 2^30 (WEXACT), lo >= -2^29 (lane_query), the window start clamped (LwWin).
-#if SVT_LW_VL && !(SVT_LW_BUF && SVT_NB_NA)
-#error "SVT_LW_VL needs SVT_LW_BUF (zero events past the span) and SVT_NB_NA (no candidate count)"
-#endif
+// One slot as vector arithmetic.  The kernel is bound by scalar issue (one SALU instruction per
+// CU and cycle): every test is the sign bit of a difference ("fail" bits), OR-ed per lane; the
+// band is one unsigned compare whose lane mask is the only ballot, and below / above accumulate
+// as sign bits in VGPRs (one ballot each per window).  Exact: the operands' ranges keep every
+// difference inside int32 -- walk positions and candidate values <= 2^30 + 2^28 + 1 (IX_SAT, one
+// op < 2^28), endpos in [1, 2^30) (slow reads carry no events), e < 2^30 (WEXACT),
+// lo >= -2^29 (lane_query), the window start clamped (LwWin).
 struct LwWin {
     int32_t b1;     // max(s - 1, -2^30) + 1: the overlap test endpos > s - 1 is endpos - b1 >= 0
     uint32_t e;
@@ -1301,25 +1265,19 @@ __device__ __forceinline__ uint64_t slot_vl(const uint4 &v, const LwWin &W, uint
     return ballot((d | fail << 31) < W.wb);
 }
 
+// The window's scalar inputs (base address of its span, span length, LwWin, lo, its staging
+// row) come from the caller's v_readlane of per-lane values computed once per wave.  Every lane
+// stores in every slot -- members to their row slot, the others to their own sink word -- so a
+// slot costs no exec-mask round trip on the scalar unit.
 template <int KIND>
-__device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, uint32_t e, uint64_t E0, uint32_t len,
-                                              int32_t lo, int32_t hi, uint16_t *row) {
-    const int32_t beg32 = (int32_t)(uint32_t)(s - 1u);
+__device__ __forceinline__ LaneBand lane_walk(uint64_t evaddr, uint32_t len, const LwWin &W, int32_t lo, uint16_t *row,
+                                              uint16_t *sink) {
     const int ln = lane_id();
-    const uint4 *ev = (KIND == K_INS ? P.spI : P.spD) + E0;   // wave-uniform base: 32-bit lane offsets
-    uint64_t below = 0, above = 0;   // candidates at or below lo / at or above hi
-    int32_t n = 0, nb = 0;
-#if SVT_LW_VL
+    int32_t nb = 0;
     uint32_t belv = 0, abv = 0;
-    const LwWin W{max(beg32, -(1 << 30)) + 1, e, (int32_t)min(s, 0x7fffffffu), lo + 1, hi - 1, (uint32_t)(hi - lo - 1)};
-#endif
-#if SVT_LW_BUF
-    const uint64_t evaddr = reinterpret_cast<uint64_t>(ev);
-#endif
     for (uint32_t b = 0; b < len; b += LW_U * WAVE) {
         const uint32_t left = len - b;
         uint4 v[LW_U];
-#if SVT_LW_BUF
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             reinterpret_cast<void *>(evaddr + (uint64_t)b * 16u), (short)0, (int)(left * 16u), 0x00020000);
 #pragma unroll
@@ -1327,167 +1285,23 @@ __device__ __forceinline__ LaneBand lane_walk(const DevPileup &P, uint32_t s, ui
             const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, ln * 16 + u * WAVE * 16, 0, 0);
             v[u] = make_uint4(r.x, r.y, r.z, r.w);
         }
-#else
-#pragma unroll
-        for (int u = 0; u < LW_U; u++)   // unconditional (clamped): all four in flight at once
-            v[u] = ev[min(b + (uint32_t)(u * WAVE + ln), len - 1u)];
-#endif
 #pragma unroll
         for (int u = 0; u < LW_U; u++) {
             if ((uint32_t)(u * WAVE) >= left) break;
-#if SVT_LW_VL
             int32_t iv;
             const uint64_t mb = slot_vl<KIND>(v[u], W, belv, abv, iv);
-#else
-            uint64_t brk;
-            uint64_t cm = span_cand_mask<KIND>(v[u], s, e, beg32, brk);
-#endif
-#if !SVT_LW_BUF
-            const uint32_t rem = left - (uint32_t)(u * WAVE);
-            if (rem < (uint32_t)WAVE) {   // the span's last, partial slot: its lanes only
-                const uint64_t in = (1ull << rem) - 1ull;
-                cm &= in;
-                brk &= in;
-            }
-#endif
-#if !SVT_LW_VL
-            const int32_t iv = (int32_t)(KIND == K_END ? ((v[u].y & 0xfu) == OP_DEL ? v[u].x + (v[u].y >> 4) + 1u
-                                                                                   : v[u].w + 1u)
-                                                       : v[u].x);
-#if !SVT_NB_NA
-            n += (int32_t)__popcll(cm | brk);
-#endif
-            above |= brk;
-            const uint64_t gt = ballot(iv > lo), lt = ballot(iv < hi);
-            below |= cm & ~gt;
-            above |= cm & ~lt;
-            const uint64_t mb = cm & gt & lt;
-#endif
-            // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone)
-            if (__builtin_amdgcn_inverse_ballot_w64(mb)) row[min(nb + (int32_t)mbcnt(mb), LV_CAP)] = (uint16_t)(iv - lo);
+            // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone);
+            // the slot is computed by every lane (the empty asm keeps the compiler from moving it
+            // under a branch on the member mask), then one select
+            uint32_t at = (uint32_t)min(nb + (int32_t)mbcnt(mb), LV_CAP);
+            asm volatile("" : "+v"(at));
+            uint16_t *dst = __builtin_amdgcn_inverse_ballot_w64(mb) ? row + at : sink;
+            *dst = (uint16_t)(iv - lo);
             nb += (int32_t)__popcll(mb);
         }
     }
-#if SVT_LW_VL
-    below = ballot((int32_t)belv < 0);
-    above = ballot((int32_t)abv < 0);
-#endif
-    return LaneBand{n, nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
-}
-
-#ifndef SVT_LV_STREAM
-#define SVT_LV_STREAM 0
-#endif
-#ifndef SVT_LV_SMAX
-#define SVT_LV_SMAX 512
-#endif
-// SVT_LV_STREAM: the windows of WAVE < len <= LV_SMAX span events (cfg4: ~93 % of the walked
-// windows, ~130 events each) are walked as ONE stream of 64-event slots -- each window's span in
-// ceil(len / 64) slots, the windows one after another -- with LV_SQ slots in flight across
-// window boundaries.  lane_walk issues a window's loads, waits for them and only then goes on
-// to the next window: one memory round trip per window, and a wave walks ~24 of them (phase
-// attribution, profiles/r05_I: the walk is 86 % of a wave's time).  Here the loads of the next
-// windows' slots are already in flight while a window's last slots are tested.  The issue side
-// and the test side each keep a cursor (window, slot) over the same sequence; a slot past the
-// stream's end is a load through a zero-size buffer descriptor (zeros, no memory access), so
-// every step issues exactly one load and the waits stay fixed.
-// Off by default: correct, but slower -- cfg4 refine 0.724-0.735 vs 0.617-0.619 ms, rank 3 of 8
-// 0.133 vs 0.106 ms (profiles/r05_K); the walk's per-wave time did not drop (phase attribution
-// unchanged), so the per-window round trip was not what held it, and the two cursors' scalar
-// work is extra issue on a kernel bound by it.
-constexpr uint32_t LV_SMAX = SVT_LV_SMAX;
-static_assert(LV_SMAX > WAVE && LV_SMAX % WAVE == 0, "LV_SMAX: whole slots, more than one");
-template <int W>
-__device__ __forceinline__ void lane_stream(const DevPileup &P, LaneLds<W> &L, uint64_t mid, uint32_t total, int32_t bw) {
-    const int ln = lane_id();
-    // issue cursor: windows not yet opened, the open window's next slot / slot count, its span
-    uint64_t mi = mid;
-    uint32_t is = 0, ins = 0, ilen = 0;
-    uint64_t ibase = reinterpret_cast<uint64_t>(P.spD);
-    auto issue = [&](uint4 &dst) {
-        if (is == ins) {
-            if (mi) {
-                const uint32_t c = (uint32_t)__builtin_ctzll(mi);
-                mi &= mi - 1ull;
-                const LvWin *wp = &L.win[c];
-                const uint32_t kind = (uint32_t)uniform_i((int32_t)wp->kl) & 0xffu;
-                const uint64_t e0 = (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)wp->e0) |
-                                    (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)(wp->e0 >> 32)) << 32;
-                ilen = (uint32_t)uniform_i((int32_t)wp->len);
-                ibase = reinterpret_cast<uint64_t>((kind == (uint32_t)K_INS ? P.spI : P.spD) + e0);
-                ins = (ilen + (uint32_t)WAVE - 1u) / (uint32_t)WAVE;
-            } else {
-                ilen = 0;
-                ins = 0;
-            }
-            is = 0;
-        }
-        const uint32_t at = is * (uint32_t)WAVE;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void *>(ibase + (uint64_t)at * 16u), (short)0, (int)(ilen > at ? (ilen - at) * 16u : 0u), 0x00020000);
-        const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, ln * 16, 0, 0);
-        dst = make_uint4(r.x, r.y, r.z, r.w);
-        is++;
-    };
-    // test cursor: the same sequence
-    uint64_t mp = mid;
-    uint32_t ps = 0, pns = 0, pkind = 0, pkw = 0;
-    int32_t plo = 0, nb = 0;
-    uint32_t belv = 0, abv = 0;
-    LwWin Wn{0, 0, 0, 0, 0, 0};
-    auto test = [&](const uint4 &v) {
-        if (ps == pns) {   // the next window opens
-            if (!mp) return;   // (the last step's slots past the stream's end)
-            const uint32_t c = (uint32_t)__builtin_ctzll(mp);
-            mp &= mp - 1ull;
-            const LvWin *wp = &L.win[c];
-            const uint32_t kl = (uint32_t)uniform_i((int32_t)wp->kl);
-            const uint32_t s = (uint32_t)uniform_i((int32_t)wp->s), e = (uint32_t)uniform_i((int32_t)wp->e);
-            const uint32_t len = (uint32_t)uniform_i((int32_t)wp->len);
-            plo = uniform_i(wp->lo);
-            pkind = kl & 0xffu;
-            pkw = kl >> 8;
-            const int32_t beg32 = (int32_t)(uint32_t)(s - 1u), hi = plo + 2 * bw;
-            Wn = LwWin{max(beg32, -(1 << 30)) + 1, e, (int32_t)min(s, 0x7fffffffu), plo + 1, hi - 1, (uint32_t)(hi - plo - 1)};
-            pns = (len + (uint32_t)WAVE - 1u) / (uint32_t)WAVE;
-            ps = 0;
-            nb = 0;
-            belv = 0;
-            abv = 0;
-        }
-        int32_t iv;
-        uint64_t mb;
-        if (pkind == (uint32_t)K_INS) mb = slot_vl<K_INS>(v, Wn, belv, abv, iv);
-        else if (pkind == (uint32_t)K_START) mb = slot_vl<K_START>(v, Wn, belv, abv, iv);
-        else mb = slot_vl<K_END>(v, Wn, belv, abv, iv);
-        uint16_t *row = L.stage + pkw * LV_S;
-        // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone)
-        if (__builtin_amdgcn_inverse_ballot_w64(mb)) row[min(nb + (int32_t)mbcnt(mb), LV_CAP)] = (uint16_t)(iv - plo);
-        nb += (int32_t)__popcll(mb);
-        if (++ps == pns) {   // the window's last slot: its meta row (as lane_walk's caller writes it)
-            const bool below = ballot((int32_t)belv < 0) != 0ull, above = ballot((int32_t)abv < 0) != 0ull;
-            if (ln == 0) {
-                L.meta[pkw].flags = nb > LV_CAP ? LV_REDO | LV_WHY(3)
-                                                : (uint32_t)nb | LV_PENDING | (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u);
-                L.meta[pkw].n = 0;
-            }
-        }
-    };
-    uint4 r0, r1, r2, r3;   // LV_SQ = 4 slots in flight, a static ring
-    issue(r0);
-    issue(r1);
-    issue(r2);
-    issue(r3);
-    for (uint32_t u = 0; u < total; u += 4) {   // (no early exits: the waits stay static)
-        test(r0);
-        issue(r0);
-        test(r1);
-        issue(r1);
-        test(r2);
-        issue(r2);
-        test(r3);
-        issue(r3);
-    }
+    const uint64_t below = ballot((int32_t)belv < 0), above = ballot((int32_t)abv < 0);
+    return LaneBand{nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
 }
 
 // One 64-event slot holding the whole spans of consecutive walkable windows win[c0..]: bit i of
@@ -1528,40 +1342,14 @@ __device__ __forceinline__ void lane_packed(const DevPileup &P, const LvWin *win
         const bool below = (cm & ~gt & rm) != 0ull, above = ((brk | (cm & ~lt)) & rm) != 0ull;
         meta[k].flags = nb > (uint32_t)LV_CAP ? (LV_REDO | LV_WHY(3))
                                               : nb | LV_PENDING | (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u);
-        meta[k].n = SVT_NB_NA ? 0 : (int32_t)__popcll((cm | brk) & rm);
+        meta[k].n = 0;
     }
 }
 
-template <int N>
-__device__ __forceinline__ void lane_sort(uint32_t (&x)[LV_CAP]) {   // ascending bitonic network, static indices
-#pragma unroll
-    for (int k = 2; k <= N; k <<= 1)
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1)
-#pragma unroll
-            for (int i = 0; i < N; i++) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const uint32_t p = x[i], q = x[l];
-                    if ((i & k) == 0) { x[i] = min(p, q); x[l] = max(p, q); }
-                    else { x[i] = max(p, q); x[l] = min(p, q); }
-                }
-            }
-}
-
-#ifndef SVT_LV_OEM
-#define SVT_LV_OEM 1
-#endif
-#ifndef SVT_LV_PREFILL
-#define SVT_LV_PREFILL 1
-#endif
-#ifndef SVT_LV_L0REG
-#define SVT_LV_L0REG 1
-#endif
-// SVT_LV_PREFILL: phase 0 fills every window's band slots with 0xffff, so phase 2 takes its
-// band straight from the row (no per-slot test against the band size).
-// SVT_LV_OEM: Batcher's odd-even merge sort instead of the bitonic network (19 / 63 / 191
-// compare-exchanges for 8 / 16 / 32 elements against 24 / 80 / 240, all ascending).
+// Phase 0 fills every window's band slots with 0xffff, so phase 2 takes its band straight from
+// the row (no per-slot test against the band size).  The band is sorted by Batcher's odd-even
+// merge sort (19 / 63 / 191 compare-exchanges for 8 / 16 / 32 elements against 24 / 80 / 240 for
+// the bitonic network, all ascending).
 __device__ __forceinline__ void lv_cx(uint32_t (&x)[LV_CAP], int i, int j) {
     const uint32_t p = x[i], q = x[j];
     x[i] = min(p, q);
@@ -1660,123 +1448,6 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int3
     return distL < distR ? valL : valR;                                      // :100
 }
 
-#ifndef SVT_VOTE_FLAT
-#define SVT_VOTE_FLAT 0
-#endif
-// lane_vote as flat loops of wave-uniform trip count (SVT_VOTE_FLAT): every step of a pass is
-// one trip -- start the next element (the break test and the cluster bookkeeping of
-// refinement.c:58-64 / :80-86), then either one cluster extension or the evaluation
-// (:65-76 / :87-97) -- with predicated updates instead of divergent branches, so the loops
-// cost no exec-mask bookkeeping on the scalar unit (the kernel's bound).  Same values as
-// lane_vote, element by element.
-// Lane predicates as all-ones / zero VGPR words behind an empty asm (the compiler cannot fold
-// them back into lane masks, whose logic would run on the scalar unit); sel() is one v_bfi.
-__device__ __forceinline__ uint32_t vm(bool c) {
-    uint32_t m = c ? 0xffffffffu : 0u;
-    asm("" : "+v"(m));
-    return m;
-}
-__device__ __forceinline__ int32_t sel(uint32_t m, int32_t a, int32_t b) {
-    return (int32_t)(((uint32_t)a & m) | ((uint32_t)b & ~m));
-}
-__device__ __forceinline__ int32_t lane_vote_flat(const uint16_t *B, int32_t nb, int32_t w, int32_t lo, uint32_t fl,
-                                                  const KParams &k, bool active) {
-    const int32_t ci = k.ci, range = k.range;
-    // elements <= pos + 25 (lower_bound, refinement.c:3-10): a fixed binary search of the <= 32
-    int32_t l0 = 0;
-#pragma unroll
-    for (int st = 32; st > 0; st >>= 1) {
-        const int32_t j = l0 + st;
-        const int32_t bj = B[min(j, LV_CAP) - 1];
-        l0 = sel(vm(j <= nb) & vm(bj <= w + SV_MIN_LENGTH / 2), j, l0);
-    }
-    const bool below = fl & LV_BELOW, above = fl & LV_ABOVE;
-    const bool u0 = !below && l0 == 0;                                          // none <= pos+25
-    const bool lt = below || (nb > 0 && (int32_t)B[0] < w - SV_MIN_LENGTH / 2);   // some < pos-25
-    int32_t p = u0 ? 0 : l0 == 0 ? -1 : l0 - 1;
-    if (nb == 0) p = -1;
-    int32_t valL = -1, maxL = k.min_count - 1, distL = 0x7fffffff;
-    int32_t valR = -1, maxR = k.min_count - 1, distR = 0x7fffffff;
-    int32_t res = 0;
-    uint32_t ret = 0;
-    {   // left pass, refinement.c:58: element i from p down, its cluster [kk, i], sum S
-        int32_t i = p, kk = p + 1, a = 0, prev = 0, S = 0;
-        uint32_t act = vm(active && i >= 0), fresh = 0xffffffffu;
-        while (ballot(act != 0u)) {
-            const int32_t bi = B[max(i, 0)];
-            const uint32_t st = act & fresh;
-            const uint32_t brk = st & vm(ref_abs(w - bi) >= range);
-            act &= ~brk;
-            const uint32_t go = st & ~brk;   // element i starts
-            S = sel(go & vm(i < p), S - prev, S);
-            const uint32_t rs = go & vm(kk > i);
-            S = sel(rs, bi, S);
-            kk = sel(rs, i, kk);
-            a = sel(go, bi, a);
-            fresh &= ~go;
-            const int32_t bk = B[max(kk - 1, 0)];
-            const uint32_t ext = act & vm(kk > 0) & vm(bk >= a - ci);          // :61-64
-            kk = sel(ext, kk - 1, kk);
-            S = sel(ext, S + bk, S);
-            const uint32_t ev = act & ~ext;
-            const int32_t c = max(i - kk + 1, 1);
-            const int32_t co = (int32_t)div_small((uint32_t)S + (uint32_t)(c / 2), (uint32_t)c);   // :65
-            const int32_t d = ref_abs(w - co);
-            const uint32_t cnt = ev & vm(c > maxL);                           // :67-76
-            const uint32_t hit = cnt & vm(d < ci);
-            const uint32_t upd = cnt & ~hit & vm(d < distL);
-            ret |= hit;
-            res = sel(hit, lo + co, res);
-            maxL = sel(upd, c, maxL);
-            valL = sel(upd, lo + co, valL);
-            distL = sel(upd, d, distL);
-            prev = sel(ev, a, prev);
-            i = sel(ev, i - 1, i);
-            fresh |= ev;
-            act &= ~hit & ~(ev & vm(i < 0));
-        }
-    }
-    {   // right pass, :80: from the full multiset's upper_bound(pos-25) up, cluster [i, m)
-        const int32_t q = lt ? (!below ? 0 : nb) : (!above ? nb - 1 : nb);
-        int32_t i = q, m = q, a = 0, prev = 0, S = 0;
-        uint32_t act = vm(active && q >= 0 && q < nb) & ~ret, fresh = 0xffffffffu;
-        while (ballot(act != 0u)) {
-            const int32_t bi = B[min(i, LV_CAP)];
-            const uint32_t st = act & fresh;
-            const uint32_t brk = st & vm(ref_abs(w - bi) >= range);
-            act &= ~brk;
-            const uint32_t go = st & ~brk;
-            S = sel(go & vm(i > q), S - prev, S);
-            const uint32_t rs = go & vm(m <= i);
-            S = sel(rs, bi, S);
-            m = sel(rs, i + 1, m);
-            a = sel(go, bi, a);
-            fresh &= ~go;
-            const int32_t bm = B[min(m, LV_CAP)];
-            const uint32_t ext = act & vm(m < nb) & vm(bm <= a + ci);          // :83-86
-            m = sel(ext, m + 1, m);
-            S = sel(ext, S + bm, S);
-            const uint32_t ev = act & ~ext;
-            const int32_t c = max(m - i, 1);
-            const int32_t co = (int32_t)div_small((uint32_t)S + (uint32_t)(c / 2), (uint32_t)c);   // :87
-            const int32_t d = ref_abs(w - co);
-            const uint32_t cnt = ev & vm(c > maxR);                           // :88-97
-            const uint32_t hit = cnt & vm(d < ci);
-            const uint32_t upd = cnt & ~hit & vm(d < distR);
-            ret |= hit;
-            res = sel(hit, lo + co, res);
-            maxR = sel(upd, c, maxR);
-            valR = sel(upd, lo + co, valR);
-            distR = sel(upd, d, distR);
-            prev = sel(ev, a, prev);
-            i = sel(ev, i + 1, i);
-            fresh |= ev;
-            act &= ~hit & ~(ev & vm(i >= nb));
-        }
-    }
-    return ret ? res : distL < distR ? valL : valR;                          // :100
-}
-
 // A2 (audit.c:176-225) for window g: kind (-1: none -> NA), s, e, pos of the vote.
 __device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &li, uint32_t &w, int32_t &chrom,
                                          uint32_t &s, uint32_t &e, uint32_t &imp) {
@@ -1856,8 +1527,8 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
     if (lo >= hi) return;
     const uint64_t *off = q.kind == K_INS ? P.spoffI : P.spoffD;
     const uint64_t E0 = off[lo], E1 = off[hi];
-    // spans of 2^31 events or more (2^27 with the buffer walk): the wave-wide path
-    if (E1 - E0 >= (SVT_LW_BUF ? (uint64_t)LW_BUF_MAX : 0x80000000ull)) { q.kind |= LQ_REDO; return; }
+    // spans of 2^27 events or more: the wave-wide path (lane_walk's buffer byte count)
+    if (E1 - E0 >= (uint64_t)LW_BUF_MAX) { q.kind |= LQ_REDO; return; }
     q.e0[0] = (uint32_t)E0; q.e0[1] = (uint32_t)(E0 >> 32);
     q.len = (uint32_t)(E1 - E0);
 }
@@ -1898,11 +1569,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         if (mine) lane_query(a, g0 + (uint32_t)ln, band_ok, q);
         const bool walk = mine && q.kind >= 0 && !(q.kind & LQ_REDO) && q.len != 0u;
         if (mine) {
-#if SVT_LV_PREFILL
             uint32_t *row32 = reinterpret_cast<uint32_t *>(L.stage + (uint32_t)ln * LV_S);
 #pragma unroll
             for (int j = 0; j < LV_CAP / 2; j++) row32[j] = 0xffffffffu;   // unused band slots read as 0xffff
-#endif
             LvMeta m;
             m.lo = q.lo;
             m.liw = q.liw;
@@ -1937,9 +1606,22 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         return;
     }
     // ---- phase 1 (packed): windows of <= 64 events share slots (lane_packed), longer ones are
-    // walked alone (lane_walk); their lengths sit in a VGPR, read by the scalar loop
+    // walked alone (lane_walk).  Lane c holds walkable window c's walk constants, computed here
+    // once for the wave; the scalar window loop reads them with v_readlane (no LDS round trip and
+    // no scalar arithmetic per window), and a window walked alone leaves its flags in lane kw of
+    // aflags (a v_cndmask on the lane index) instead of a store to its meta row.
+    uint32_t aflags = 0;
     {
-        const uint32_t lenv = (uint32_t)ln < nwin ? L.win[ln].len : 0u;
+        const bool has = (uint32_t)ln < nwin;
+        const LvWin wv = L.win[has ? (uint32_t)ln : 0u];   // (entry 0 unused when nwin == 0)
+        const uint32_t lenv = has ? wv.len : 0u, klv = wv.kl, ev = wv.e;
+        const int32_t lov = wv.lo;
+        const int32_t b1v = max((int32_t)(wv.s - 1u), -(1 << 30)) + 1;
+        const int32_t scv = (int32_t)min(wv.s, 0x7fffffffu);
+        const uint64_t addrv =
+            reinterpret_cast<uint64_t>(((klv & 0xffu) == (uint32_t)K_INS ? a.pile.spI : a.pile.spD) + wv.e0);
+        uint16_t *sink = reinterpret_cast<uint16_t *>(&L.sink[ln]);
+        const int32_t bw2 = 2 * bw;
 #if SVT_PHASE_PROF
         if (ln == 0) PH_ADD(8, nwin);
         {
@@ -1954,28 +1636,18 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             if (ln == 0 && l0 <= (uint32_t)WAVE) PH_ADD(12, 1);
 #endif
             if (l0 > (uint32_t)WAVE) {
-#if SVT_LV_STREAM
-                if (l0 <= LV_SMAX) {   // lane_stream's
-                    c++;
-                    continue;
-                }
-#endif
-                const LvWin *wp = &L.win[c];
-                const uint32_t kl = (uint32_t)uniform_i((int32_t)wp->kl);
-                const uint32_t s = (uint32_t)uniform_i((int32_t)wp->s), e = (uint32_t)uniform_i((int32_t)wp->e);
-                const int32_t lo = uniform_i(wp->lo);
-                const uint64_t E0 = (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)wp->e0) |
-                                    (uint64_t)(uint32_t)uniform_i((int32_t)(uint32_t)(wp->e0 >> 32)) << 32;
-                const uint32_t kind = kl & 0xffu, kw = kl >> 8;
+                const uint32_t kl = rdlane(klv, (int)c), kind = kl & 0xffu, kw = kl >> 8;
+                const int32_t lo = rdlane_i(lov, (int)c);
+                const LwWin W{rdlane_i(b1v, (int)c), rdlane(ev, (int)c), rdlane_i(scv, (int)c), lo + 1, lo + bw2 - 1,
+                              (uint32_t)(bw2 - 1)};
+                const uint64_t base = rdlane64(addrv, (int)c);
                 uint16_t *row = L.stage + kw * LV_S;
                 LaneBand r;
-                if (kind == (uint32_t)K_INS) r = lane_walk<K_INS>(a.pile, s, e, E0, l0, lo, lo + 2 * bw, row);
-                else if (kind == (uint32_t)K_START) r = lane_walk<K_START>(a.pile, s, e, E0, l0, lo, lo + 2 * bw, row);
-                else r = lane_walk<K_END>(a.pile, s, e, E0, l0, lo, lo + 2 * bw, row);
-                if (ln == 0) {
-                    L.meta[kw].flags = r.nb > LV_CAP ? LV_REDO | LV_WHY(3) : (uint32_t)r.nb | LV_PENDING | r.flags;
-                    L.meta[kw].n = r.n;
-                }
+                if (kind == (uint32_t)K_INS) r = lane_walk<K_INS>(base, l0, W, lo, row, sink);
+                else if (kind == (uint32_t)K_START) r = lane_walk<K_START>(base, l0, W, lo, row, sink);
+                else r = lane_walk<K_END>(base, l0, W, lo, row, sink);
+                const uint32_t f = r.nb > LV_CAP ? (LV_REDO | LV_WHY(3)) : (uint32_t)r.nb | LV_PENDING | r.flags;
+                aflags = (uint32_t)ln == kw ? f : aflags;
                 c++;
                 continue;
             }
@@ -1987,29 +1659,21 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 M |= 1ull << tot;
                 tot += l;
             }
-            lane_packed(a.pile, L.win, L.meta, L.stage, c, M, tot, 2 * bw);
+            lane_packed(a.pile, L.win, L.meta, L.stage, c, M, tot, bw2);
             c = c1;
         }
-#if SVT_LV_STREAM
-        {
-            const bool md = (uint32_t)ln < nwin && lenv > (uint32_t)WAVE && lenv <= LV_SMAX;
-            const uint64_t mid = ballot(md);
-            if (mid) {
-                const uint32_t total = rdlane(wave_scan_add(md ? (lenv + (uint32_t)WAVE - 1u) / (uint32_t)WAVE : 0u), WAVE - 1);
-                lane_stream<LV_W>(a.pile, L, mid, total, bw);
-            }
-        }
-#endif
         wave_sync();
     }
 #if SVT_PHASE_PROF
     const long long pt2 = wall_clock64();
 #endif
+    const bool mine = (uint32_t)ln < cnt;
+    LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0};
+    if (aflags) mt.flags = aflags;   // the window was walked alone
     if (SVT_DIAG == 8) {   // diagnostic build: phases 0-1 only (a checksum of their LDS output written out)
-        if ((uint32_t)ln < cnt) {
-            const LvMeta mt = L.meta[ln];
+        if (mine) {
             const uint32_t *row32 = reinterpret_cast<const uint32_t *>(L.stage + (uint32_t)ln * LV_S);
-            uint32_t h = mt.flags ^ (uint32_t)mt.n ^ (uint32_t)mt.lo;
+            uint32_t h = mt.flags ^ (uint32_t)mt.lo;
             for (int j = 0; j < LV_S / 2; j++) h = h * 31u + row32[j];
             write_result(a, mt.liw >> 1, mt.liw & 1u, h);
         }
@@ -2018,12 +1682,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     // ---- phase 2: one lane per staged window
     uint64_t redo;   // phase 3's windows (the meta rows are overwritten by its gathers)
     {
-        const bool mine = (uint32_t)ln < cnt;
-        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0};
-        // decisions: no window or fewer than min_count candidates -> NA (refinement.c:43-45);
-        // the wave-wide path; or this lane's vote
-        const bool na = mine && ((mt.flags & LV_NONE) ||
-                                 (!(mt.flags & LV_REDO) && (SVT_NB_NA ? (int32_t)(mt.flags & 0xffu) : mt.n) < k.min_count));
+        // decisions: no window or fewer than min_count band members -> NA (refinement.c:43-45,
+        // LaneBand); the wave-wide path; or this lane's vote
+        const bool na = mine && ((mt.flags & LV_NONE) || (!(mt.flags & LV_REDO) && (int32_t)(mt.flags & 0xffu) < k.min_count));
         if (na) write_result(a, mt.liw >> 1, mt.liw & 1u, SVT_NA);
         redo = ballot(mine && !na && (mt.flags & LV_REDO));
         const bool pend = mine && !na && !(mt.flags & LV_REDO) && (mt.flags & LV_PENDING);
@@ -2037,13 +1698,8 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
 #pragma unroll
             for (int j = 0; j < LV_CAP; j += 2) {   // two offsets per 4-byte LDS read
                 const uint32_t v = row32[j >> 1];
-#if SVT_LV_PREFILL
                 x[j] = v & 0xffffu;   // (slots past the band hold 0xffff: phase 0)
                 x[j + 1] = v >> 16;
-#else
-                x[j] = j < nb ? (v & 0xffffu) : 0xffffu;
-                x[j + 1] = j + 1 < nb ? (v >> 16) : 0xffffu;
-#endif
             }
             int32_t nmax = nb;   // wave max of nb: the smallest network that sorts every lane
 #pragma unroll
@@ -2051,37 +1707,20 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
 #if SVT_PHASE_PROF
             if (ln == 0) PH_ADD(nmax <= 8 ? 13 : nmax <= 16 ? 14 : 15, 1);
 #endif
-#if SVT_LV_OEM
             if (nmax <= 8) lv_oe_sort<0, 8>(x);
             else if (nmax <= 16) lv_oe_sort<0, 16>(x);
             else lv_oe_sort<0, 32>(x);
-#else
-            if (nmax <= 8) lane_sort<8>(x);
-            else if (nmax <= 16) lane_sort<16>(x);
-            else lane_sort<32>(x);
-#endif
             uint32_t *wrow = reinterpret_cast<uint32_t *>(row);
             if (pend) {
 #pragma unroll
                 for (int j = 0; j < LV_CAP; j += 2) wrow[j >> 1] = x[j] | x[j + 1] << 16;
-#if SVT_VOTE_FLAT
-            }
-            {
-                const int32_t r = lane_vote_flat(row, nb, bw, mt.lo, mt.flags, k, pend);
-                if (pend) write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
-#else
-#if SVT_LV_L0REG
                 // the band elements <= pos + 25, counted on the sorted registers (no search)
                 int32_t l0 = 0;
 #pragma unroll
                 for (int j = 0; j < LV_CAP; j++) l0 += (int32_t)(x[j] <= (uint32_t)(bw + SV_MIN_LENGTH / 2));
                 l0 = min(l0, nb);
                 const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k, l0);
-#else
-                const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k);
-#endif
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
-#endif
             }
         }
         wave_sync();
@@ -2091,8 +1730,6 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
 #endif
     // ---- the windows voted wave-wide go to refine_redo_kernel (rare: 0.6 % of cfg4's)
     if (SVT_DIAG == 11) {   // diagnostic build: each left-over window's result = 0xF0000000 | its reason
-        const bool mine = (uint32_t)ln < cnt;
-        const LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0};
         if ((redo >> ln) & 1ull) write_result(a, mt.liw >> 1, mt.liw & 1u, 0xF0000000u | (mt.flags >> 16));
         return;
     }
@@ -3422,25 +3059,27 @@ void svt_host_free(svt_ctx *c, void *p) {
 // ---- BAM records decoded on the device (svt_bam.inc)
 }  // extern "C"
 
-// SVT_FEED_PARTS: svt_bam_dec_feed copies a batch's compressed bytes in up to this many parts on
-// a copy stream, and inflates part k while part k + 1 crosses PCIe (the batch's blocks are
-// independent); 1 (default): copy, then inflate.  4 parts measured slower end to end on cfg2
-// (3.54 vs 2.12 s, device feeds 3.04 vs 1.70 s, profiles/r05_I).
-#ifndef SVT_FEED_PARTS
-#define SVT_FEED_PARTS 1
-#endif
-constexpr int FEED_PARTS = SVT_FEED_PARTS;
-constexpr size_t FEED_PART_MIN = 256;   // blocks a part at least (each part is one inflate launch)
+// svt_bam_dec_feed is pipelined one batch deep: a call copies its batch's compressed bytes to the
+// device (a copy stream, into one of two input buffers) while the previous batch still inflates,
+// then decodes the previous batch (whose carried tail fixes where this batch's bytes go) and
+// launches this batch's inflate; the next call or svt_bam_dec_load decodes it.  (Copying a batch in
+// parts beside its own inflate measured slower: every part's launch waits for its slowest block,
+// profiles/r05_I.)
 struct svt_bam_dec {
     svt_ctx *c = nullptr;
     int32_t n_ref = 0;
     hipStream_t st = nullptr;
     hipStream_t cst = nullptr;                // the copy stream
-    hipEvent_t pev[FEED_PARTS] = {};          // part k's bytes are on the device
-    uint8_t *d_comp = nullptr;
-    size_t comp_cap = 0;
-    svt_bgzf_block *d_blk = nullptr;
-    size_t blk_cap = 0;
+    hipEvent_t cev = nullptr;                 // the latest batch's bytes are on the device
+    uint8_t *d_comp[2] = {nullptr, nullptr};  // compressed batches (alternating)
+    size_t comp_cap[2] = {0, 0};
+    svt_bgzf_block *d_blk[2] = {nullptr, nullptr};
+    size_t blk_cap[2] = {0, 0};
+    int ib = 0;                               // the next batch's input buffer
+    uint32_t *d_err = nullptr;                // the inflate's first bad block (this decoder's own word)
+    bool pend = false;                        // a batch inflated (or inflating) but not yet decoded
+    size_t pend_n = 0;
+    uint64_t pend_u = 0, pend_r0 = 0;
     uint8_t *d_buf[2] = {nullptr, nullptr};   // inflated batches: [carried tail | this batch]
     size_t buf_cap[2] = {0, 0};
     int cur = 0;
@@ -3486,70 +3125,28 @@ svt_status svt_bam_dec_open(svt_ctx *c, int32_t n_targets, svt_bam_dec **out) {
     if (!d) return fail(c, SVT_ENOMEM, "%s", "host memory");
     d->c = c;
     d->n_ref = n_targets;
-    bool ok = hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking) == hipSuccess &&
-              hipMalloc(&d->d_chk, sizeof(BdCheck)) == hipSuccess;
-    for (auto &e : d->pev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    const bool ok = hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) == hipSuccess &&
+                    hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking) == hipSuccess &&
+                    hipEventCreateWithFlags(&d->cev, hipEventDisableTiming) == hipSuccess &&
+                    hipMalloc(&d->d_chk, sizeof(BdCheck)) == hipSuccess && hipMalloc(&d->d_err, sizeof(uint32_t)) == hipSuccess;
     if (!ok) {
         svt_bam_dec_close(d);
         return fail(c, SVT_EDEVICE, "%s", "BAM decode: stream / buffers");
-    }
-    if (!c->d_inferr && hipMalloc(&c->d_inferr, sizeof(uint32_t)) != hipSuccess) {
-        svt_bam_dec_close(d);
-        return fail(c, SVT_ENOMEM, "%s", "inflate scratch");
     }
     *out = d;
     return SVT_OK;
 }
 
-svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
-                            size_t n, uint64_t skip) {
-    if (!d) return SVT_EINVAL;
+namespace {
+// The pending batch's records: it was inflated into d_buf[cur] after the carried tail (its
+// kernels run on d->st, so the decode's launches wait for them).  The incomplete last record
+// moves to the front of the other buffer.
+svt_status bd_decode(svt_bam_dec *d) {
     svt_ctx *c = d->c;
-    if (n && (!comp || !blocks)) return fail(c, SVT_EINVAL, "%s", "null buffer");
-    if (n > 0xfffffffeull) return fail(c, SVT_EINVAL, "%s", "more than 2^32 - 2 blocks in one call");
-    uint64_t U = 0;
-    for (size_t i = 0; i < n; i++) {   // every block inside its buffers (the kernel trusts the table)
-        const svt_bgzf_block &k = blocks[i];
-        if (k.clen > 65536u || k.ulen > 65536u || k.coff > comp_bytes || k.clen > comp_bytes - k.coff)
-            return fail(c, SVT_EINVAL, "%s", "BGZF block outside its buffers (or over 64 KiB)");
-        U = std::max<uint64_t>(U, k.uoff + k.ulen);
-    }
-    DEV_GUARD(c);
-    using clk = std::chrono::steady_clock;
-    const clk::time_point t0 = clk::now();
     svt_status s;
-    const uint64_t T = d->tail, N = T + U;
-    const uint64_t r0 = d->first ? skip : 0;
-    if (r0 > N) return fail(c, SVT_EINVAL, "%s", "BAM decode: the header runs past the first batch");
-    if ((s = bd_grow(c, d->d_comp, d->comp_cap, comp_bytes + 64)) || (s = bd_grow(c, d->d_blk, d->blk_cap, std::max<size_t>(n, 1))) ||
-        (s = bd_grow(c, d->d_buf[d->cur], d->buf_cap[d->cur], N + 64, T)))
-        return s;
+    d->pend = false;
     uint8_t *buf = d->d_buf[d->cur];
-    if (n) {
-        // the error word is the context's: order this call after its other streams' calls
-        if ((s = order_on(c, d->st))) return s;
-        HIP_TRY(c, hipMemsetAsync(c->d_inferr, 0xff, sizeof(uint32_t), d->st));
-        // the parts: consecutive blocks, each part's bytes the span its blocks cover (the previous
-        // call's inflates are done: it synchronised d->st before returning)
-        const size_t np = std::max<size_t>(1, std::min<size_t>((size_t)FEED_PARTS, n / FEED_PART_MIN));
-        HIP_TRY(c, hipMemcpyAsync(d->d_blk, blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->cst));
-        for (size_t p = 0; p < np; p++) {
-            const size_t b0 = n * p / np, b1 = n * (p + 1) / np;
-            uint64_t lo = ~0ull, hi = 0;
-            for (size_t i = b0; i < b1; i++) {
-                lo = std::min<uint64_t>(lo, blocks[i].coff);
-                hi = std::max<uint64_t>(hi, blocks[i].coff + blocks[i].clen);
-            }
-            if (hi > lo) HIP_TRY(c, hipMemcpyAsync(d->d_comp + lo, comp + lo, hi - lo, hipMemcpyHostToDevice, d->cst));
-            HIP_TRY(c, hipEventRecord(d->pev[p], d->cst));
-            HIP_TRY(c, hipStreamWaitEvent(d->st, d->pev[p], 0));
-            const unsigned grid = (unsigned)std::min<size_t>(b1 - b0, (size_t)INF_GRID);
-            hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, d->st, d->d_comp, d->d_blk, (uint32_t)b0,
-                               (uint32_t)(b1 - b0), buf + T, c->d_inferr);
-            HIP_TRY(c, hipGetLastError());
-        }
-    }
+    const uint64_t N = d->tail + d->pend_u, r0 = d->pend_r0;
     const uint64_t span = N - r0;
     const uint32_t nch = (uint32_t)((span + BD_CHUNK - 1) / BD_CHUNK);
     BdCheck chk{1u, 0u, 0ull, N, 0u, 0u, 0ull};
@@ -3560,9 +3157,9 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
         HIP_TRY(c, hipGetLastError());
         uint32_t ierr = 0xffffffffu;
         HIP_TRY(c, hipMemcpyAsync(&chk, d->d_chk, sizeof chk, hipMemcpyDeviceToHost, d->st));
-        HIP_TRY(c, hipMemcpyAsync(&ierr, c->d_inferr, sizeof ierr, hipMemcpyDeviceToHost, d->st));
+        HIP_TRY(c, hipMemcpyAsync(&ierr, d->d_err, sizeof ierr, hipMemcpyDeviceToHost, d->st));
         HIP_TRY(c, hipStreamSynchronize(d->st));
-        if (n && ierr != 0xffffffffu) {
+        if (d->pend_n && ierr != 0xffffffffu) {
             char m[64];
             snprintf(m, sizeof m, "%u", ierr);
             return fail(c, SVT_EINVAL, "corrupt BGZF block %s of the batch (does not inflate to its ISIZE)", m);
@@ -3636,7 +3233,61 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
     HIP_TRY(c, hipStreamSynchronize(d->st));
     d->cur = nx;
     d->tail = nt;
+    return SVT_OK;
+}
+}  // namespace
+
+svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_bytes, const svt_bgzf_block *blocks,
+                            size_t n, uint64_t skip) {
+    if (!d) return SVT_EINVAL;
+    svt_ctx *c = d->c;
+    if (n && (!comp || !blocks)) return fail(c, SVT_EINVAL, "%s", "null buffer");
+    if (n > 0xfffffffeull) return fail(c, SVT_EINVAL, "%s", "more than 2^32 - 2 blocks in one call");
+    uint64_t U = 0, lo = ~0ull, hi = 0;
+    for (size_t i = 0; i < n; i++) {   // every block inside its buffers (the kernel trusts the table)
+        const svt_bgzf_block &k = blocks[i];
+        if (k.clen > 65536u || k.ulen > 65536u || k.coff > comp_bytes || k.clen > comp_bytes - k.coff)
+            return fail(c, SVT_EINVAL, "%s", "BGZF block outside its buffers (or over 64 KiB)");
+        U = std::max<uint64_t>(U, k.uoff + k.ulen);
+        lo = std::min<uint64_t>(lo, k.coff);
+        hi = std::max<uint64_t>(hi, k.coff + k.clen);
+    }
+    DEV_GUARD(c);
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    svt_status s;
+    const uint64_t r0 = d->first ? skip : 0;   // (the first batch carries no tail)
+    if (r0 > (d->first ? 0 : d->tail) + U) return fail(c, SVT_EINVAL, "%s", "BAM decode: the header runs past the first batch");
     d->first = false;
+    // this batch's bytes cross PCIe while the previous batch inflates (its input is the other buffer)
+    const int ib = d->ib;
+    d->ib ^= 1;
+    if ((s = bd_grow(c, d->d_comp[ib], d->comp_cap[ib], comp_bytes + 64)) ||
+        (s = bd_grow(c, d->d_blk[ib], d->blk_cap[ib], std::max<size_t>(n, 1))))
+        return s;
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(d->d_blk[ib], blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->cst));
+        if (hi > lo) HIP_TRY(c, hipMemcpyAsync(d->d_comp[ib] + lo, comp + lo, hi - lo, hipMemcpyHostToDevice, d->cst));
+        HIP_TRY(c, hipEventRecord(d->cev, d->cst));
+    }
+    // the previous batch's records: fixes the carried tail this batch's bytes follow
+    if (d->pend && (s = bd_decode(d))) return s;
+    const uint64_t T = d->tail, N = T + U;
+    if ((s = bd_grow(c, d->d_buf[d->cur], d->buf_cap[d->cur], N + 64, T))) return s;
+    if (n) {
+        if ((s = order_on(c, d->st))) return s;
+        HIP_TRY(c, hipMemsetAsync(d->d_err, 0xff, sizeof(uint32_t), d->st));
+        HIP_TRY(c, hipStreamWaitEvent(d->st, d->cev, 0));
+        const unsigned grid = (unsigned)std::min<size_t>(n, (size_t)INF_GRID);
+        hipLaunchKernelGGL(inflate_kernel, dim3(grid), dim3(WAVE), 0, d->st, d->d_comp[ib], d->d_blk[ib], 0u, (uint32_t)n,
+                           d->d_buf[d->cur] + T, d->d_err);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipEventSynchronize(d->cev));   // the caller may reuse its buffers
+    }
+    d->pend = true;
+    d->pend_n = n;
+    d->pend_u = U;
+    d->pend_r0 = r0;
     d->stats.batches++;
     d->stats.inflated_bytes += U;
     d->stats.feed_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
@@ -3661,9 +3312,15 @@ svt_status svt_bam_dec_stats_get(const svt_bam_dec *d, svt_bam_dec_stats *out) {
 svt_status svt_bam_dec_load(svt_bam_dec *d) {
     if (!d) return SVT_EINVAL;
     svt_ctx *c = d->c;
-    if (d->tail) return fail(c, SVT_EINVAL, "%s", "truncated BAM record at end of file");
     DEV_GUARD(c);
     using clk = std::chrono::steady_clock;
+    if (d->pend) {   // the last batch's records
+        const clk::time_point tf = clk::now();
+        const svt_status sd = bd_decode(d);
+        d->stats.feed_ms += std::chrono::duration<double, std::milli>(clk::now() - tf).count();
+        if (sd) return sd;
+    }
+    if (d->tail) return fail(c, SVT_EINVAL, "%s", "truncated BAM record at end of file");
     const clk::time_point t0 = clk::now();
     free_pileup(c);
     c->load_stats = svt_load_stats{};
@@ -3751,13 +3408,13 @@ void svt_bam_dec_close(svt_bam_dec *d) {
         // the context's launch order may point at this stream (svt_bam_dec_feed's order_on): all of
         // its work is done, so nothing later has to wait for it, and it must not be named again
         if (d->c->have_last && d->c->last_stream == d->st) d->c->have_last = false;
-        hfree(d->d_comp); hfree(d->d_blk); hfree(d->d_buf[0]); hfree(d->d_buf[1]);
+        if (d->cst) (void)hipStreamSynchronize(d->cst);
+        hfree(d->d_comp[0]); hfree(d->d_comp[1]); hfree(d->d_blk[0]); hfree(d->d_blk[1]); hfree(d->d_err);
+        hfree(d->d_buf[0]); hfree(d->d_buf[1]);
         hfree(d->d_ch); hfree(d->d_base); hfree(d->d_rec); hfree(d->d_pre); hfree(d->d_chk); hfree(d->d_tmp);
         hfree(d->cols.tid); hfree(d->cols.pos); hfree(d->cols.endpos); hfree(d->cols.nc); hfree(d->cols.soff);
         hfree(d->cols.stream);
-        if (d->cst) (void)hipStreamSynchronize(d->cst);
-        for (auto &e : d->pev)
-            if (e) (void)hipEventDestroy(e);
+        if (d->cev) (void)hipEventDestroy(d->cev);
         if (d->st) (void)hipStreamDestroy(d->st);
         if (d->cst) (void)hipStreamDestroy(d->cst);
     }

@@ -37,6 +37,9 @@ def main() -> int:
                     help="the CPU baseline's sample instead of the whole workload: the first K loci of contig 1 "
                          "(genomic order) and the BAM of their region, with SEQ/QUAL -- the same bytes bench.py's "
                          "cpu_baseline BGZF leg times (oracle/bgzf_baseline.py)")
+    ap.add_argument("--libs", default="tree",
+                    help="engine builds to time on the same files, comma-separated: 'tree' the in-tree libsvtrek_hip.so, "
+                         "else a directory holding a variant libsvtrek_hip.so (LD_LIBRARY_PATH); reps alternate between them")
     a = ap.parse_args()
 
     import numpy as np
@@ -60,37 +63,45 @@ def main() -> int:
     prep = time.perf_counter() - t
     cli = os.path.join(ROOT, "svtrek_amd", "svtrek")
     outs = {}
+    libs = a.libs.split(",")
     for mode in a.inflate.split(","):
-        times = []
+        times = {lb: [] for lb in libs}
+        stages = {}
         for _ in range(a.reps):
-            t = time.perf_counter()
-            env = dict(os.environ)
-            if ":" in mode:
-                env["SVTREK_INFLATE_BATCH_MB"] = mode.split(":")[1]
-            base = mode.split(":")[0]
-            if base == "gpuhost":
-                env["SVTREK_HOSTPARSE"] = "1"
-            p = subprocess.run([cli, "audt", "-b", bam, "-v", vcf, "-t", str(a.t), "--verbose", "--inflate",
-                                "gpu" if base == "gpuhost" else base], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                               timeout=1800, env=env)
-            times.append(time.perf_counter() - t)
-            if p.returncode != 0:
-                print(p.stderr.decode()[-2000:], file=sys.stderr)
-                return p.returncode
-        outs[mode] = p.stdout
-        lines = p.stdout.count(b"\n") - 2
-        stages = [l for l in p.stderr.decode(errors="replace").splitlines() if l.startswith("[svtrek_amd]")]
-        best = min(times)
-        print(json.dumps({
-            "metric": "end-to-end svtrek audt (BAM ingest + H2D + refine + print)", "workload": a.workload,
-            "inflate": mode, "loci": int(len(loci)), "printed_records": int(lines), "bam_bytes": os.path.getsize(bam),
-            "with_seq": a.with_seq or bool(a.region_sample), "host_threads": a.t, "seconds_best": round(best, 3),
-            "seconds_all": [round(x, 3) for x in times], "loci_per_s": round(len(loci) / best, 1),
-            "region_sample": {"loci": a.region_sample, "region": region} if a.region_sample else None,
-            "disk_free_gb_before": round(free_gb, 1),
-            "prep_seconds": round(prep, 1), "stages_last_run": stages[-1] if stages else None}), flush=True)
+            for lb in libs:
+                env = dict(os.environ)
+                if lb != "tree":
+                    env["LD_LIBRARY_PATH"] = os.path.abspath(lb)
+                if ":" in mode:
+                    env["SVTREK_INFLATE_BATCH_MB"] = mode.split(":")[1]
+                base = mode.split(":")[0]
+                if base == "gpuhost":
+                    env["SVTREK_HOSTPARSE"] = "1"
+                t = time.perf_counter()
+                p = subprocess.run([cli, "audt", "-b", bam, "-v", vcf, "-t", str(a.t), "--verbose", "--inflate",
+                                    "gpu" if base == "gpuhost" else base], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                   timeout=1800, env=env)
+                times[lb].append(time.perf_counter() - t)
+                if p.returncode != 0:
+                    print(p.stderr.decode()[-2000:], file=sys.stderr)
+                    return p.returncode
+                outs[(mode, lb)] = p.stdout
+                st = [l for l in p.stderr.decode(errors="replace").splitlines() if l.startswith("[svtrek_amd]")]
+                stages[lb] = st[-1] if st else None
+        for lb in libs:
+            lines = outs[(mode, lb)].count(b"\n") - 2
+            best = min(times[lb])
+            print(json.dumps({
+                "metric": "end-to-end svtrek audt (BAM ingest + H2D + refine + print)", "workload": a.workload,
+                "inflate": mode, "engine": "in-tree" if lb == "tree" else lb, "loci": int(len(loci)),
+                "printed_records": int(lines), "bam_bytes": os.path.getsize(bam),
+                "with_seq": a.with_seq or bool(a.region_sample), "host_threads": a.t, "seconds_best": round(best, 3),
+                "seconds_all": [round(x, 3) for x in times[lb]], "loci_per_s": round(len(loci) / best, 1),
+                "region_sample": {"loci": a.region_sample, "region": region} if a.region_sample else None,
+                "disk_free_gb_before": round(free_gb, 1),
+                "prep_seconds": round(prep, 1), "stages_last_run": stages[lb]}), flush=True)
     if len(outs) > 1 and len(set(outs.values())) != 1:
-        print("stdout differs between inflate modes", file=sys.stderr)
+        print("stdout differs between inflate modes / engine builds", file=sys.stderr)
         return 1
     return 0
 
