@@ -142,3 +142,27 @@ def test_wrong_guess_rechains_from_the_failing_chunk(engine_factory, tmp_path):
     st = _same_as_host(engine_factory, path, _loci(np.random.default_rng(41), 3))
     n_chunks = (len(body) + 65535) // 65536
     assert st["rechained"] == 1 and 0 < st["rechained_chunks"] < n_chunks
+
+
+@pytest.mark.parametrize("which", ["middle", "last"])
+def test_corrupt_block_reported_by_the_pipelined_feed(engine_factory, tmp_path, which):
+    """svt_bam_dec_feed is pipelined one batch deep: a batch's inflate error is found by the call
+    that decodes it (the next feed, or svt_bam_dec_load for the last batch).  A block whose ISIZE
+    claims one byte more than its DEFLATE data holds must fail the load either way."""
+    import struct
+    raw, recs = bamfix.make_bam(seed=23, n_reads=3000, unplaced=0)
+    data = bytearray(bamfix.bgzf_blocks(raw))
+    starts, p = [], 0
+    while p + 18 <= len(data):   # BGZF members: BSIZE at offset 16
+        starts.append(p)
+        p += struct.unpack_from("<H", data, p + 16)[0] + 1
+    assert p == len(data) and len(starts) >= 6
+    b = starts[len(starts) // 2] if which == "middle" else starts[-2]   # (starts[-1]: the EOF block)
+    end = b + struct.unpack_from("<H", data, b + 16)[0] + 1
+    isize = struct.unpack_from("<I", data, end - 4)[0]
+    struct.pack_into("<I", data, end - 4, isize + 1)
+    path = str(tmp_path / f"c_{which}.bam")
+    with open(path, "wb") as f:
+        f.write(bytes(data))
+    with pytest.raises((OSError, SvtError), match="corrupt"):
+        host.load_bam_device(engine_factory(), path, batch_bytes=64 << 10)
