@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.23.2 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.23.3 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -1304,6 +1304,54 @@ __device__ __forceinline__ LaneBand lane_walk(uint64_t evaddr, uint32_t len, con
     return LaneBand{nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
 }
 
+// Two windows of the same kind with 65-128 span events each, walked together: their four slots'
+// loads are in flight at once, so the pair costs one memory round trip instead of two (phase 1
+// is a chain of one round trip per window per wave, ~24 a wave on cfg4).
+struct LwOne {
+    uint64_t base;
+    uint32_t len;
+    LwWin W;
+    int32_t lo;
+    uint16_t *row;
+};
+template <int KIND>
+__device__ __forceinline__ void lane_walk2(const LwOne &A, const LwOne &B, uint16_t *sink, LaneBand &ra, LaneBand &rb) {
+    const int ln = lane_id();
+    const __amdgpu_buffer_rsrc_t sa = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A.base), (short)0,
+                                                                        (int)(A.len * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t sb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(B.base), (short)0,
+                                                                        (int)(B.len * 16u), 0x00020000);
+    uint4 v[4];
+    {
+        const u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(sa, ln * 16, 0, 0);
+        const u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(sa, ln * 16 + WAVE * 16, 0, 0);
+        const u32x4 r2 = __builtin_amdgcn_raw_buffer_load_b128(sb, ln * 16, 0, 0);
+        const u32x4 r3 = __builtin_amdgcn_raw_buffer_load_b128(sb, ln * 16 + WAVE * 16, 0, 0);
+        v[0] = make_uint4(r0.x, r0.y, r0.z, r0.w);
+        v[1] = make_uint4(r1.x, r1.y, r1.z, r1.w);
+        v[2] = make_uint4(r2.x, r2.y, r2.z, r2.w);
+        v[3] = make_uint4(r3.x, r3.y, r3.z, r3.w);
+    }
+#pragma unroll
+    for (int w = 0; w < 2; w++) {
+        const LwOne &O = w ? B : A;
+        int32_t nb = 0;
+        uint32_t belv = 0, abv = 0;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            int32_t iv;
+            const uint64_t mb = slot_vl<KIND>(v[2 * w + u], O.W, belv, abv, iv);
+            uint32_t at = (uint32_t)min(nb + (int32_t)mbcnt(mb), LV_CAP);
+            asm volatile("" : "+v"(at));
+            uint16_t *dst = __builtin_amdgcn_inverse_ballot_w64(mb) ? O.row + at : sink;
+            *dst = (uint16_t)(iv - O.lo);
+            nb += (int32_t)__popcll(mb);
+        }
+        const uint64_t below = ballot((int32_t)belv < 0), above = ballot((int32_t)abv < 0);
+        (w ? rb : ra) = LaneBand{nb, (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u)};
+    }
+}
+
 // One 64-event slot holding the whole spans of consecutive walkable windows win[c0..]: bit i of
 // M marks the first lane of a window (bit 0 always), tot <= 64 events in all.  Lane j walks
 // event j - f of the window that starts at f = the highest mark <= j, with that window's own
@@ -1635,6 +1683,29 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             if (ln == 0 && l0 > (uint32_t)WAVE) { PH_ADD(10, 1); PH_ADD(11, (l0 + 255u) / 256u); }
             if (ln == 0 && l0 <= (uint32_t)WAVE) PH_ADD(12, 1);
 #endif
+            if (l0 > (uint32_t)WAVE && l0 <= 2u * WAVE && c + 1u < nwin) {   // a pair of 2-slot windows?
+                const uint32_t l1 = rdlane(lenv, (int)(c + 1u));
+                const uint32_t ka = rdlane(klv, (int)c), kb = rdlane(klv, (int)(c + 1u));
+                if (l1 > (uint32_t)WAVE && l1 <= 2u * WAVE && ((ka ^ kb) & 0xffu) == 0u) {
+                    auto one = [&](uint32_t cc, uint32_t kl, uint32_t len) {
+                        const int32_t lo = rdlane_i(lov, (int)cc);
+                        return LwOne{rdlane64(addrv, (int)cc), len,
+                                     LwWin{rdlane_i(b1v, (int)cc), rdlane(ev, (int)cc), rdlane_i(scv, (int)cc), lo + 1,
+                                           lo + bw2 - 1, (uint32_t)(bw2 - 1)},
+                                     lo, L.stage + (kl >> 8) * LV_S};
+                    };
+                    const LwOne A = one(c, ka, l0), B = one(c + 1u, kb, l1);
+                    LaneBand ra, rb;
+                    if ((ka & 0xffu) == (uint32_t)K_INS) lane_walk2<K_INS>(A, B, sink, ra, rb);
+                    else if ((ka & 0xffu) == (uint32_t)K_START) lane_walk2<K_START>(A, B, sink, ra, rb);
+                    else lane_walk2<K_END>(A, B, sink, ra, rb);
+                    const uint32_t fa = ra.nb > LV_CAP ? (LV_REDO | LV_WHY(3)) : (uint32_t)ra.nb | LV_PENDING | ra.flags;
+                    const uint32_t fb = rb.nb > LV_CAP ? (LV_REDO | LV_WHY(3)) : (uint32_t)rb.nb | LV_PENDING | rb.flags;
+                    aflags = (uint32_t)ln == (ka >> 8) ? fa : (uint32_t)ln == (kb >> 8) ? fb : aflags;
+                    c += 2u;
+                    continue;
+                }
+            }
             if (l0 > (uint32_t)WAVE) {
                 const uint32_t kl = rdlane(klv, (int)c), kind = kl & 0xffu, kw = kl >> 8;
                 const int32_t lo = rdlane_i(lov, (int)c);
