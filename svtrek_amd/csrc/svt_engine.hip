@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.23.3 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.23.4 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
