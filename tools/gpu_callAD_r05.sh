@@ -7,6 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT=gpurun_out/r05_AD
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+mkdir -p /tmp/e2e_c2 /tmp/e2e_c4
 summ() {
   python - "$1" "$2" <<'PY'
 import json, sys
@@ -26,4 +27,7 @@ for pin in 0 1; do
     --reps 3 --inflate gpu --dir /tmp/e2e_c4 > "$OUT/e2e_c4_pin$pin.log" 2>&1 || { echo "e2e c4 failed"; tail -5 "$OUT/e2e_c4_pin$pin.log"; exit 1; }
   summ "pin$pin" "$OUT/e2e_c4_pin$pin.log"
 done
+timeout -k 10 700 python -u tools/e2e_shard.py --world 8 --ranks 0,3,7 -t 16 --reps 2 > "$OUT/e2e_shard.log" 2>&1 \
+  || { echo "e2e shard failed"; tail -5 "$OUT/e2e_shard.log"; exit 1; }
+tail -4 "$OUT/e2e_shard.log" | cut -c1-600
 echo done
