@@ -240,7 +240,7 @@ def dry_run(args, world: int, rank: int) -> int:
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     if rank == 0:
-        parts = [p.numpy().view(np.uint32).reshape(-1, 4) for p in pg.gathered((args.steps - 1) % 2)]
+        parts = [p.numpy().view(np.uint32).reshape(-1, 4) for p in pg.gathered(args.steps - 1)]
         unpack_records(np.concatenate(parts), n_total)
         ranks_seen = sum(int((p[:, 0] != 0xFFFFFFFF).any()) for p in parts)
         print(json.dumps({
@@ -274,8 +274,8 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="steps in flight (1 or 2): 2 engine contexts and streams, step i + 1's index build beside "
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="steps in flight (1-4): K engine contexts and streams, step i + 1's index build beside "
                          "step i's refine")
     ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records check")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -338,7 +338,7 @@ def main() -> int:
     # K steps in flight (--inflight K): K engine contexts, each with the pileup and its own index
     # buffers, and K streams; step i runs on context / stream i % K, so step i + 1's index build
     # overlaps step i's refine.  Every step is the whole work (index build + refine of all loci).
-    K = max(1, min(2, args.inflight))
+    K = max(1, min(4, args.inflight))
     engs = [Engine(params, device=dev.index) for _ in range(K)]
     t0 = time.perf_counter()
     for e_ in engs:
@@ -359,7 +359,7 @@ def main() -> int:
     sh = stream.cuda_stream
     gather = world > 1 and not args.no_gather
     pg = PipelinedGather(lambda: torch.full((rec_words,), -1, dtype=torch.int32, device=dev),   # pads: index ~0
-                         world, rank, enabled=gather)   # (two buffers: buffer i % 2 <-> context i % K)
+                         world, rank, enabled=gather, nbuf=K)   # (buffer i % max(K, 2) <-> context i % K)
 
     def launch(i: int, k: int = 0) -> None:
         engs[k].refine_device_records(d_loci.data_ptr(), n, pg.buffer(i).data_ptr(), d_index.data_ptr(), 0,
@@ -410,7 +410,7 @@ def main() -> int:
         t_max = float(tt.item())
 
     # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records)
-    last = (args.steps - 1) % 2
+    last = args.steps - 1
     verified = None
     gather_ranks = None
     if rank == 0 and (gather or world == 1) and not args.no_verify and not args.emulate_shard:

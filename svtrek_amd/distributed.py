@@ -80,22 +80,24 @@ def unpack_records(recs: np.ndarray, n_total: int) -> np.ndarray:
 
 
 class PipelinedGather:
-    """Double-buffered gather of per-step record buffers to rank 0 (bench.py's N > 1 step).
+    """Multi-buffered gather of per-step record buffers to rank 0 (bench.py's N > 1 step).
 
-    `buffer(i)` hands out step i's buffer (waiting -- as a stream dependency on GPU backends --
-    for the gather that last read it), `submit(i)` starts its asynchronous gather, so the
-    gather of step i overlaps the refinement launch of step i + 1."""
+    `buffer(i)` hands out step i's buffer, i % nbuf (waiting -- as a stream dependency on GPU
+    backends -- for the gather that last read it), `submit(i)` starts its asynchronous gather, so
+    the gather of step i overlaps the refinement launches of the next steps.  nbuf >= the steps
+    in flight: no two steps in flight write one buffer."""
 
-    def __init__(self, make_buf, world: int, rank: int, enabled: bool = True, group=None):
+    def __init__(self, make_buf, world: int, rank: int, enabled: bool = True, group=None, nbuf: int = 2):
         import torch
-        self.bufs = [make_buf(), make_buf()]
+        self.n = max(2, int(nbuf))
+        self.bufs = [make_buf() for _ in range(self.n)]
         self.lists = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in self.bufs]
-        self.handles = [None, None]
+        self.handles = [None] * self.n
         self.enabled = enabled and world > 1
         self.group = group
 
     def buffer(self, i: int):
-        b = i % 2
+        b = i % self.n
         if self.handles[b] is not None:
             self.handles[b].wait()
             self.handles[b] = None
@@ -104,11 +106,11 @@ class PipelinedGather:
     def submit(self, i: int) -> None:
         if self.enabled:
             import torch.distributed as dist
-            b = i % 2
+            b = i % self.n
             self.handles[b] = dist.gather(self.bufs[b], self.lists[b], dst=0, group=self.group, async_op=True)
 
     def drain(self) -> None:
-        for b in range(2):
+        for b in range(self.n):
             if self.handles[b] is not None:
                 self.handles[b].wait()
                 self.handles[b] = None
@@ -116,8 +118,8 @@ class PipelinedGather:
     def gathered(self, i: int):
         """Rank 0: the buffers every rank sent at step i (after drain()); else None."""
         if not self.enabled:
-            return [self.bufs[i % 2]]
-        return self.lists[i % 2]
+            return [self.bufs[i % self.n]]
+        return self.lists[i % self.n]
 
 
 def gather_results(rows: np.ndarray, local: np.ndarray, n_total: int, device=None,
