@@ -195,7 +195,7 @@ def launch_ranks(n: int, argv: list[str]) -> int:
 def dry_run(args, world: int, rank: int) -> int:
     """`--dry-run`: the N-rank plumbing of the bench on the CPU (gloo), no engine. Each rank
     shards the seeded workload exactly as the GPU run does, writes its slice's 16-B records
-    (the loci unrefined: start = end = NA) into the double-buffered gather for K steps, and
+    (the loci unrefined: start = end = NA) into the multi-buffered gather for K steps, and
     rank 0 checks that every VCF row arrived exactly once and prints the one JSON line. It
     measures nothing (value is the plumbing's own rate) -- it exists so that the launcher, the
     rank environment and the gather are exercised without a GPU (tests/test_distributed.py)."""
@@ -221,7 +221,7 @@ def dry_run(args, world: int, rank: int) -> int:
     local["end"] = SVT_NA
     recs = torch.from_numpy(pack_records(rows, local, per).view(np.int32).reshape(-1).copy())
     pg = PipelinedGather(lambda: torch.full((per * RECORD_DTYPE.itemsize // 4,), -1, dtype=torch.int32),
-                         world, rank, enabled=world > 1)
+                         world, rank, enabled=world > 1, nbuf=max(1, min(4, args.inflight)))   # (as the GPU run's)
     for i in range(args.warmup):
         pg.buffer(i).copy_(recs)
         pg.submit(i)

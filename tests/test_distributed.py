@@ -272,3 +272,23 @@ def test_bench_launcher_stops_ranks_on_failure():
     r = subprocess.run([sys.executable, bench, "--gpus", "2", "--dry-run", "--workload", "nope"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+@pytest.mark.parametrize("nbuf", [1, 2, 3, 4])
+def test_pipelined_gather_one_buffer_per_step_in_flight(nbuf):
+    """bench.py gives the gather one buffer per step in flight (--inflight K, at least two): steps
+    i and i + 1 .. i + K - 1 never share a buffer, and gathered(i) is step i's."""
+    import torch
+    from svtrek_amd.distributed import PipelinedGather
+    pg = PipelinedGather(lambda: torch.zeros(4, dtype=torch.int32), 1, 0, enabled=False, nbuf=nbuf)
+    k = max(2, nbuf)
+    assert pg.n == k
+    for i in range(3 * k):
+        pg.buffer(i).fill_(i)
+        for j in range(max(0, i - k + 1), i):
+            assert pg.buffer(j).data_ptr() != pg.buffer(i).data_ptr()
+            pg.buffer(j).fill_(j)   # (restore: buffer(j) is handed out again above)
+        pg.submit(i)
+    pg.drain()
+    last = 3 * k - 1
+    assert int(pg.gathered(last)[0][0]) == last
