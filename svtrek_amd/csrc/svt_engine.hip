@@ -356,7 +356,8 @@ __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141:
 
 #ifndef SVT_DIAG
 #define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 3 = no refine_end
-                                 // stop search, 4 = no sort/vote, 5 = sort + prefix sums, no vote
+                                 // stop search, 4 = no sort/vote, 5 = sort + prefix sums, no vote, ...,
+                                 // 23 = the lane emit without its CIGAR walk (svt_index2.inc, profiles/r05_AK)
 #endif
 
 
