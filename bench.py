@@ -132,6 +132,57 @@ def _engine_version() -> str:
     return version()
 
 
+def engine_lib_identity() -> dict:
+    """The engine library this process binds (path relative to the repo, sha256, and whether
+    SVTREK_ENGINE_LIB named a variant build) -- so an A/B variant cannot pass as the product."""
+    import hashlib
+    from svtrek_amd._lib import engine_path
+    path = engine_path()
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return {"path": os.path.relpath(os.path.realpath(path), ROOT), "sha256": h.hexdigest(),
+            "override": bool(os.environ.get("SVTREK_ENGINE_LIB"))}
+
+
+def parity_sample(parts, res, first_rows, n_random: int = 10000, seed: int = 0, threads: int = 8,
+                  full: bool = False) -> dict:
+    """Untimed self-check of the timed records (the checker, like cpu_baseline: the only other bench
+    use of oracle/): the records of the last step -- `parts`, the gathered {vcf_index, start, end,
+    pad} buffers -- against the CPU oracle (refinement.c:327-339 restated) on the rows of the
+    cpu_baseline sample (`first_rows`) plus a seeded random sample of n_random of the rows the
+    records hold (every row with full=True).  Returns {"loci", "mismatches", ...}."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ffi as O  # noqa: E402
+    from svtrek_amd.distributed import PAD_INDEX
+    rec = np.concatenate([np.asarray(p).reshape(-1, 4) for p in parts]).astype(np.uint32)
+    rec = rec[rec[:, 0] != PAD_INDEX]
+    if full:
+        pick = np.arange(len(rec))
+    else:
+        pos = np.full(len(res.loci), -1, dtype=np.int64)
+        pos[rec[:, 0].astype(np.int64)] = np.arange(len(rec))
+        want = np.asarray(first_rows, dtype=np.int64)
+        want = want[pos[want] >= 0]
+        rng = np.random.default_rng(seed)
+        rnd = rng.choice(len(rec), size=min(n_random, len(rec)), replace=False)
+        pick = np.unique(np.concatenate([pos[want], rnd]))
+    rows = rec[pick, 0].astype(np.int64)
+    want = O.refine_batch(res.pileup, res.loci[rows], threads=threads)
+    bad = np.nonzero((rec[pick, 1] != want["start"]) | (rec[pick, 2] != want["end"]))[0]
+    out = {"loci": int(len(rows)), "mismatches": int(len(bad)),
+           "sample": ("every row the records hold" if full else
+                      f"the cpu_baseline sample's rows + {min(n_random, len(rec))} seeded random rows (seed {seed})"),
+           "oracle": "oracle/svtrek_oracle.c (CPU restatement of refinement.c / audit.c)"}
+    if len(bad):
+        k = int(bad[0])
+        out["first"] = {"vcf_row": int(rows[k]), "got": [int(rec[pick[k], 1]), int(rec[pick[k], 2])],
+                        "want": [int(want["start"][k]), int(want["end"][k])]}
+    return out
+
+
 STEP_KERNELS = ("ix2_census_kernel", "ix2_emit_kernel", "refine_lane_kernel", "refine_redo_kernel")
 STREAM_INDEX_KERNELS = ("index_kernel", "ix_copy_kernel")   # the long-read index build (svt_index.inc)
 
@@ -216,9 +267,15 @@ def dry_run(args, world: int, rank: int) -> int:
     res = sim.generate(cfg)
     rows, sl, spile = shard_workload(res.loci, res.pileup, Params(), world, rank)
     n_total, per = len(res.loci), padded_rows(len(res.loci), world)
-    local = np.zeros(len(sl), dtype=RESULT_DTYPE)
-    local["start"] = SVT_NA
-    local["end"] = SVT_NA
+    # the records: the CPU oracle's results for the slice (a stand-in for the engine, so the
+    # parity self-check below has real records to check; nothing here is timed as refinement)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ffi as O  # noqa: E402
+    local = O.refine_batch(spile, sl, threads=2) if len(sl) else np.zeros(0, dtype=RESULT_DTYPE)
+    if args.corrupt_record is not None and rank == world - 1 and len(sl):   # (tests: a mismatch fails the run)
+        local = local.copy()
+        k = args.corrupt_record % len(sl)
+        local["start"][k] = (int(local["start"][k]) + 1) & 0xFFFFFFFF
     recs = torch.from_numpy(pack_records(rows, local, per).view(np.int32).reshape(-1).copy())
     pg = PipelinedGather(lambda: torch.full((per * RECORD_DTYPE.itemsize // 4,), -1, dtype=torch.int32),
                          world, rank, enabled=world > 1, nbuf=max(1, min(4, args.inflight)))   # (as the GPU run's)
@@ -239,10 +296,13 @@ def dry_run(args, world: int, rank: int) -> int:
     tt = torch.tensor([wall], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    rc = 0
     if rank == 0:
         parts = [p.numpy().view(np.uint32).reshape(-1, 4) for p in pg.gathered(args.steps - 1)]
         unpack_records(np.concatenate(parts), n_total)
         ranks_seen = sum(int((p[:, 0] != 0xFFFFFFFF).any()) for p in parts)
+        ps = parity_sample(parts, res, np.arange(min(n_total, 200)), n_random=500, threads=2)
+        rc = 1 if ps["mismatches"] else 0
         print(json.dumps({
             "metric": "refined SV loci/sec (whole node)", "value": round(n_total * args.steps / float(tt.item()), 1),
             "unit": "loci/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -252,13 +312,18 @@ def dry_run(args, world: int, rank: int) -> int:
             "dry_run": True,
             "config": {"workload": args.workload, "loci_total": n_total, "loci_per_gpu": len(sl),
                        "parallelism": f"genomic row shard x{world}", "gather": "gloo" if world > 1 else None},
-            "gather_ranks": ranks_seen if world > 1 else 1, "records_verified": True,
+            "gather_ranks": ranks_seen if world > 1 else 1, "records_verified": rc == 0,
+            "parity_sample": ps,
+            "records_note": "the slice records are the CPU oracle's results (stand-in for the engine)",
             "cpu_baseline": None,
             "cpu_baseline_note": "not timed in a dry run",
         }), flush=True)
+        if rc:
+            print(f"bench.py: parity self-check failed: {ps['mismatches']} of {ps['loci']} sampled loci differ "
+                  f"from the oracle (first: {ps.get('first')})", file=sys.stderr, flush=True)
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 def main() -> int:
@@ -277,7 +342,15 @@ def main() -> int:
     ap.add_argument("--inflight", type=int, default=3,
                     help="steps in flight (1-4): K engine contexts and streams, step i + 1's index build beside "
                          "step i's refine")
-    ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records check")
+    ap.add_argument("--no-verify", action="store_true", help="diagnostic builds: skip the records checks")
+    ap.add_argument("--parity-full", action="store_true",
+                    help="check every timed record against the oracle (default: the cpu_baseline sample + 10k "
+                         "seeded random rows)")
+    ap.add_argument("--gather-backend", choices=("auto", "nccl", "gloo"), default="auto",
+                    help="N > 1: the gather's backend; auto = nccl (RCCL over xGMI) when every rank has its own "
+                         "GPU, else gloo through host memory (one-device emulation: ranks share device 0; not a "
+                         "scaling number)")
+    ap.add_argument("--corrupt-record", type=int, default=None, help=argparse.SUPPRESS)   # tests: dry run only
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-sample-loci", type=int, default=1000,
                     help="loci of the BGZF CPU leg's sample (the first K of contig 1, genomic order; 45000 ~ cfg4's "
@@ -309,12 +382,21 @@ def main() -> int:
     from svtrek_amd import Engine, Params, sim
     from svtrek_amd._lib import RECORD_DTYPE
     from svtrek_amd.distributed import PipelinedGather, padded_rows, shard_workload, unpack_records
+    # one GPU per rank; fewer GPUs than ranks (a one-GPU box) is the one-device emulation: the ranks
+    # share the devices round-robin and gather through host memory (gloo) -- the N-rank code path
+    # with the engine, not a scaling number
+    ndev = torch.cuda.device_count()
+    emulated = world > 1 and ndev < world
+    backend = args.gather_backend if args.gather_backend != "auto" else ("gloo" if emulated else "nccl")
+    if emulated and backend == "nccl":
+        ap.error(f"{world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank (use --gather-backend gloo)")
+    dev = torch.device("cuda", (local % ndev) if world > 1 else 0)
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     # ---- the workload (BASELINE config), identical on every rank; this rank's genomic slice
     cfg = sim.WORKLOADS[args.workload]
@@ -359,7 +441,8 @@ def main() -> int:
     sh = stream.cuda_stream
     gather = world > 1 and not args.no_gather
     pg = PipelinedGather(lambda: torch.full((rec_words,), -1, dtype=torch.int32, device=dev),   # pads: index ~0
-                         world, rank, enabled=gather, nbuf=K)   # (buffer i % max(K, 2) <-> context i % K)
+                         world, rank, enabled=gather, nbuf=K,   # (buffer i % max(K, 2) <-> context i % K)
+                         host_stage=backend == "gloo")
 
     def launch(i: int, k: int = 0) -> None:
         engs[k].refine_device_records(d_loci.data_ptr(), n, pg.buffer(i).data_ptr(), d_index.data_ptr(), 0,
@@ -405,19 +488,27 @@ def main() -> int:
 
     t_max = wall
     if world > 1:
-        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        tt = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
 
-    # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records)
+    # ---- untimed: every VCF row arrives exactly once at rank 0 (last step's records), and the
+    # records agree with the CPU oracle on a sample (the whole set with --parity-full)
     last = args.steps - 1
     verified = None
     gather_ranks = None
-    if rank == 0 and (gather or world == 1) and not args.no_verify and not args.emulate_shard:
+    parity = None
+    rc = 0
+    if rank == 0 and (gather or world == 1) and not args.no_verify:
         parts = [p.cpu().numpy().view(np.uint32).reshape(-1, 4) for p in pg.gathered(last)]
-        unpack_records(np.concatenate(parts), n_total)
+        if not args.emulate_shard:
+            unpack_records(np.concatenate(parts), n_total)
         gather_ranks = sum(int((p[:, 0] != 0xFFFFFFFF).any()) for p in parts)
-        verified = True
+        cores_ps = cpu_cores()[0]
+        parity = parity_sample(parts, res, rows[:min(len(rows), args.cpu_sample_loci)], threads=cores_ps,
+                               full=args.parity_full)
+        verified = parity["mismatches"] == 0
+        rc = 0 if verified else 1
 
     # ---- untimed: the two phases on their own (5 runs each), and a step with the Infinity
     # Cache flushed first
@@ -490,7 +581,8 @@ def main() -> int:
                        "reads_per_gpu": spile.n_reads, "cigar_ops_per_gpu": spile.n_ops,
                        "coverage": cfg.coverage, "read_len_mean": cfg.read_len_mean,
                        "parallelism": f"genomic row shard x{world}",
-                       "gather": "16-B records, RCCL gather to rank 0, overlapped with the next launch"
+                       "gather": ("16-B records, RCCL gather to rank 0, overlapped with the next launch"
+                                  if backend == "nccl" else "16-B records, gloo gather to rank 0 through host memory")
                        if gather else None,
                        **({"loci_scale": args.scale} if args.scale != 1.0 else {}),
                        **({"emulated_shard": args.emulate_shard} if args.emulate_shard else {})},
@@ -544,17 +636,24 @@ def main() -> int:
                 f"{world}" if world > 1 else "skipped (--no-cpu-baseline or an emulated shard)"}),
             "work": work,
             "records_verified": verified,
+            "parity_sample": parity,
             "gather_ranks": gather_ranks,
+            "engine_lib": engine_lib_identity(),
+            **({"emulation": f"one-device emulation: {world} ranks on {ndev} GPU(s), gather through host memory "
+                             "(gloo) -- the N-rank path with the engine, not a scaling number"} if emulated else {}),
             "setup_s": {"generate": round(gen_s, 2), "shard": round(shard_s, 2), "load_pileup": round(load_s, 2)},
             "pileup_device_bytes": eng.device_bytes,
             "engine_version": _engine_version(),
         }
         print(json.dumps(out), flush=True)
+        if rc:
+            print(f"bench.py: parity self-check failed: {parity['mismatches']} of {parity['loci']} sampled loci "
+                  f"differ from the oracle (first: {parity.get('first')})", file=sys.stderr, flush=True)
     for e_ in engs:
         e_.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

@@ -134,10 +134,18 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one GPU per rank (RCCL); with fewer GPUs than ranks the ranks share them round-robin and the
+    # status all-reduce and gather go through host memory (gloo): the one-device emulation
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    emulated = world > 1 and ndev < world
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if emulated:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     if rank == 0:
         sys.stdout.write("[INFO] Started processing variation file.\n")
         sys.stdout.flush()
@@ -154,13 +162,13 @@ def main(argv=None) -> int:
 
     def refine(pl, mine):   # the engine is built on first use, inside the guarded region too
         if "eng" not in state:
-            state["eng"] = Engine(prm, device=local)
+            state["eng"] = Engine(prm, device=gpu)
         state["eng"].load_pileup(pl)
         return state["eng"].refine(mine)
 
     rc = 0
     try:
-        res = run_rank(a.bam, load_loci, prm, max(1, a.t), refine, world, rank, device=dev)
+        res = run_rank(a.bam, load_loci, prm, max(1, a.t), refine, world, rank, device=None if emulated else dev)
     except RuntimeError as e:
         sys.stderr.write(f"[ERROR] {e}\n")
         res, rc = None, 1

@@ -124,8 +124,8 @@ constexpr int W_WINDOWS = 0, W_READS = 1, W_OPS = 2, W_CANDS = 3, W_SPILLED = 4,
               W_RANGE = 7, W_LREADS = 8, W_LENTRIES = 9, W_STOPS = 10, W_STOPCH = 11, W_SQUERIES = 12,
               W_SPAN = 13, W_N = 14;
 constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status, work counters
-constexpr size_t CTL_REDO = 200;    // two redo counters (alternating launches)
-static_assert(16 + 8 * W_N <= CTL_BYTES, "control block too small");
+constexpr size_t CTL_REDO = 200;    // redo counters: two alternating (direct launches), one + scratch (captured)
+static_assert(16 + 8 * W_N <= CTL_REDO && CTL_REDO + 16 <= CTL_BYTES, "control block too small");
 
 // ------------------------------------------------------------------ wave primitives
 #define SVT_COLD __forceinline__   // (cold paths inlined: out-of-line calls measured slower)
@@ -1920,12 +1920,13 @@ struct svt_ctx {
     uint32_t n_ranges = 0;
     IxTot *d_agg = nullptr;           // range (group) totals
     IxTot *d_bsum = nullptr, *d_bpre = nullptr;   // their sums per block of IX_BLK, the blocks' exclusive scan
+    size_t n_bsum = 0;
+    bool bsum_dirty = false;          // a build stopped between its walk (which adds into d_bsum) and the
+                                      // scan (which zeroes it again): the next build clears it first
     uint4 *d_scr = nullptr;                        // stream walk: staged events / offsets per range, overflow flags
     uint2 *d_scrh = nullptr;
     uint32_t *d_ovf = nullptr;
     uint2 *d_cnt = nullptr;           // [n_reads] lane-per-read census -> emit (svt_index2.inc)
-    uint64_t *d_ix3 = nullptr;        // single-pass lane build: [2g + q] status words of group g, list q
-    uint32_t ix3_epoch = 0;           // its builds so far (the status words' epoch)
     uint32_t n_groups = 0;            // 64-read groups of the lane-per-read index
     int ix_mode = 0;                  // index build: 0 by read length, 1 lane per read (svt_index2.inc), 2 stream
                                       // walk (svt_index.inc) -- SVTREK_IX=auto|lane|stream
@@ -1950,7 +1951,7 @@ struct svt_ctx {
     int32_t *d_pool = nullptr;
     unsigned long long pool_words = 0;
     unsigned char *d_ctl = nullptr;   // [0,8) pool head (epoch-tagged), [8,12) sticky status, [12,16) index
-                                      // build guard, [16,16+8*W_N) work, [CTL_REDO, +8) left-over counters
+                                      // build guard, [16,16+8*W_N) work, [CTL_REDO, +16) left-over counters
     uint32_t epoch = 0;               // launches so far (pool epochs cycle through 1 .. 2^24-1)
     // launches run in submission order across streams (order_on)
     hipStream_t last_stream = nullptr;
@@ -2039,7 +2040,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_pos); hfree(c->d_emax); hfree(c->d_rec); hfree(c->d_clip8); hfree(c->d_off64);
     hfree(c->d_tid_off); hfree(c->d_bkt_off); hfree(c->d_bkt); hfree(c->d_cigar);
     hfree(c->d_ins_off); hfree(c->d_ins_bases);
-    hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_bsum); hfree(c->d_bpre); hfree(c->d_tot); hfree(c->d_ix3);
+    hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_bsum); hfree(c->d_bpre); hfree(c->d_tot);
     hfree(c->d_scr); hfree(c->d_scrh); hfree(c->d_ovf);
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_spD); hfree(c->d_spI);
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
@@ -2114,15 +2115,24 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
             HIP_TRY(c, hipMalloc(&c->d_redo, 2 * n * sizeof(uint32_t)));
             c->redo_cap = 2 * n;
         }
-        // Two left-over counters alternate between lane launches: this launch appends to
-        // ctr[par]; its redo kernel reads that and zeroes ctr[par ^ 1] for the next lane launch.
-        // The parity advances on lane launches only (counting and span launches in between
-        // leave both counters alone), and both start zeroed (svt_open).
+        // Two left-over counters alternate between direct lane launches: this launch appends to
+        // ctr[par]; its redo kernel reads that and zeroes ctr[par ^ 1] for the next one.  The
+        // parity advances on direct lane launches only (counting and span launches in between leave
+        // both alone), and both start zeroed (svt_open).  A launch captured into a graph has its own
+        // counter, ctr[2], zeroed by a memset node at the head of its graph, and its redo kernel's
+        // "next" word is the scratch ctr[3]: replays run whenever the caller likes, so they must
+        // neither read nor leave state the direct launches' alternation depends on.
         a.redo_list = c->d_redo;
-        a.redo_ctr = (uint32_t *)(c->d_ctl + CTL_REDO) + c->lane_par;
-        a.redo_next = (uint32_t *)(c->d_ctl + CTL_REDO) + (c->lane_par ^ 1u);
-        c->lane_par ^= 1u;
-        if (captured) HIP_TRY(c, hipMemsetAsync(a.redo_ctr, 0, sizeof(uint32_t), st));
+        uint32_t *ctr = (uint32_t *)(c->d_ctl + CTL_REDO);
+        if (captured) {
+            a.redo_ctr = ctr + 2;
+            a.redo_next = ctr + 3;
+            HIP_TRY(c, hipMemsetAsync(a.redo_ctr, 0, sizeof(uint32_t), st));
+        } else {
+            a.redo_ctr = ctr + c->lane_par;
+            a.redo_next = ctr + (c->lane_par ^ 1u);
+            c->lane_par ^= 1u;
+        }
         // (16 windows a wave for the 250K-window launches of a 125K-locus shard measured slower:
         // 0.132-0.138 vs 0.117-0.121 ms, profiles/r04_sh)
         hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
@@ -2437,25 +2447,12 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     const dim3 grid2((unsigned)((c->n_groups + IX2_WPB - 1) / IX2_WPB)), block2(64 * IX2_WPB);
     const dim3 grid1((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block1(64 * IX_WPB);
     if (ms && hipEventRecord(ev[0], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
-    // one pass when the lists are sized -- except in a stream capture: a graph would replay the
-    // capture's epoch, which the status words of its previous replay already carry
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (lane && !first && SVT_IX2_FUSED && hipStreamIsCapturing(st, &cap) != hipSuccess)
-        return done(fail(c, SVT_EDEVICE, "%s", "hipStreamIsCapturing"));
-    if (lane && !first && SVT_IX2_FUSED && cap == hipStreamCaptureStatusNone) {
-        hipLaunchKernelGGL(ix2_fused_kernel, grid2, block2, 0, st, a2, c->ix3_epoch++, c->d_ix3);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index build: %s", hipGetErrorString(e)));
-        if (ms) {
-            float t0 = 0.f;
-            e = hipEventRecord(ev[1], st);
-            if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
-            if (e == hipSuccess) e = hipEventElapsedTime(&t0, ev[0], ev[1]);
-            if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index timing: %s", hipGetErrorString(e)));
-            *ms = (double)t0;
-        }
-        return done(SVT_OK);
+    if (c->bsum_dirty) {
+        if (hipMemsetAsync(c->d_bsum, 0, c->n_bsum * sizeof(IxTot), st) != hipSuccess)
+            return done(fail(c, SVT_EDEVICE, "%s", "index block sums: hipMemsetAsync"));
+        c->bsum_dirty = false;
     }
+    c->bsum_dirty = true;
     if (lane)
         hipLaunchKernelGGL(ix2_census_kernel, grid2, block2, 0, st, a2);
     else
@@ -2467,6 +2464,7 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
         e = hipGetLastError();
     }
     if (e != hipSuccess) return done(fail(c, SVT_EDEVICE, "index census: %s", hipGetErrorString(e)));
+    c->bsum_dirty = false;   // the scan launched: it zeroes the block sums behind itself
     if (ms && hipEventRecord(ev[1], st) != hipSuccess) return done(fail(c, SVT_EDEVICE, "%s", "hipEventRecord"));
     if (first) {
         uint64_t t[IX_NTOT];
@@ -2617,11 +2615,10 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
     if ((s = upload<IxTot>(c, c->d_bsum, nullptr, 0, NB))) return s;   // (zeroed: the first build adds into them)
     if ((s = upload<IxTot>(c, c->d_bpre, nullptr, 0, NB))) return s;
     HIP_TRY(c, hipMemset(c->d_bsum, 0, NB * sizeof(IxTot)));
+    c->n_bsum = NB;
+    c->bsum_dirty = false;
     if (c->n_ranges > 0x7fffffffu) return fail(c, SVT_EINVAL, "pileup: %s", "too many index ranges");
     if ((s = upload<uint64_t>(c, c->d_tot, nullptr, 0, IX_NTOT))) return s;
-    if ((s = upload<uint64_t>(c, c->d_ix3, nullptr, 0, 2 * std::max<size_t>((size_t)c->n_groups, 1)))) return s;
-    HIP_TRY(c, hipMemset(c->d_ix3, 0, 2 * std::max<size_t>((size_t)c->n_groups, 1) * sizeof(uint64_t)));   // no status yet
-    c->ix3_epoch = 0;
     if (!index_lane(c, nops, (uint64_t)nr)) {   // the stream walk's scratch slots
         const size_t RR = std::max<size_t>(c->n_ranges, 1);
         if ((s = upload<uint4>(c, c->d_scr, nullptr, 0, RR * IX_SCAP))) return s;
@@ -3337,7 +3334,16 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
     if ((s = bd_grow(c, d->d_comp[ib], d->comp_cap[ib], comp_bytes + 64)) ||
         (s = bd_grow(c, d->d_blk[ib], d->blk_cap[ib], std::max<size_t>(n, 1))))
         return s;
+    // Once this batch's copies are queued, every return waits for them first: the header lets the
+    // caller reuse `comp` / `blocks` as soon as the call returns, error returns included.
+    struct CopyWait {
+        hipStream_t cst = nullptr;
+        ~CopyWait() {
+            if (cst) (void)hipStreamSynchronize(cst);
+        }
+    } copy_wait;
     if (n) {
+        copy_wait.cst = d->cst;
         HIP_TRY(c, hipMemcpyAsync(d->d_blk[ib], blocks, n * sizeof(svt_bgzf_block), hipMemcpyHostToDevice, d->cst));
         if (hi > lo) HIP_TRY(c, hipMemcpyAsync(d->d_comp[ib] + lo, comp + lo, hi - lo, hipMemcpyHostToDevice, d->cst));
         HIP_TRY(c, hipEventRecord(d->cev, d->cst));
@@ -3355,6 +3361,7 @@ svt_status svt_bam_dec_feed(svt_bam_dec *d, const uint8_t *comp, size_t comp_byt
                            d->d_buf[d->cur] + T, d->d_err);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventSynchronize(d->cev));   // the caller may reuse its buffers
+        copy_wait.cst = nullptr;
     }
     d->pend = true;
     d->pend_n = n;

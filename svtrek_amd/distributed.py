@@ -87,11 +87,16 @@ class PipelinedGather:
     the gather of step i overlaps the refinement launches of the next steps.  nbuf >= the steps
     in flight: no two steps in flight write one buffer."""
 
-    def __init__(self, make_buf, world: int, rank: int, enabled: bool = True, group=None, nbuf: int = 2):
+    def __init__(self, make_buf, world: int, rank: int, enabled: bool = True, group=None, nbuf: int = 2,
+                 host_stage: bool = False):
         import torch
         self.n = max(2, int(nbuf))
         self.bufs = [make_buf() for _ in range(self.n)]
-        self.lists = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in self.bufs]
+        # host_stage (gloo with device buffers, the one-device emulation): each submit copies its
+        # buffer to host memory (waiting for the step) and gathers the host copy
+        self.host = host_stage and self.bufs[0].device.type != "cpu"
+        self.send = [torch.empty(b.shape, dtype=b.dtype) for b in self.bufs] if self.host else self.bufs
+        self.lists = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in self.send]
         self.handles = [None] * self.n
         self.enabled = enabled and world > 1
         self.group = group
@@ -107,7 +112,9 @@ class PipelinedGather:
         if self.enabled:
             import torch.distributed as dist
             b = i % self.n
-            self.handles[b] = dist.gather(self.bufs[b], self.lists[b], dst=0, group=self.group, async_op=True)
+            if self.host:
+                self.send[b].copy_(self.bufs[b])
+            self.handles[b] = dist.gather(self.send[b], self.lists[b], dst=0, group=self.group, async_op=True)
 
     def drain(self) -> None:
         for b in range(self.n):

@@ -24,3 +24,13 @@ def test_hand_built_blocks_match_zlib_verdicts():
                                  ({9: 1, 2: 2, 1: 2}, [9] * 256 + [2], [1], False)]:
         comp = D.dynamic_block(cl, lit, dist, data)
         assert D.zlib_ok(comp, len(data)) == valid
+
+
+def test_crafted_streams_decode_as_written():
+    """The crafted multi-block streams (far-edge matches, stored after dynamic blocks, chunk-end
+    outputs, long codes) inflate under zlib to exactly the bytes the writer expanded."""
+    import random
+    import zlib
+    for comp, plain, name in D.crafted_streams(random.Random(17)):
+        assert zlib.decompressobj(-15).decompress(comp) == plain, name
+        assert 0 < len(plain) <= 65536, name

@@ -248,6 +248,54 @@ def test_bench_launcher_spawns_ranks_dry_run(world):
     out = json.loads(lines[0])
     assert out["n_gpus"] == world and out["gather_ranks"] == world and out["records_verified"] is True
     assert out["config"]["loci_total"] == 100 and out["cpu_baseline"] is None
+    assert out["parity_sample"]["loci"] == 100 and out["parity_sample"]["mismatches"] == 0
+
+
+def test_bench_parity_mismatch_fails_the_run():
+    """the bench checks its own records against the oracle after the timed
+    loop -- one wrong record on the last rank (a diagnostic flag of the dry run) is reported in
+    parity_sample and the run exits non-zero."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    bench = os.path.join(os.path.dirname(here), "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, bench, "--gpus", "2", "--dry-run", "--workload", "cfg1_100del_10x",
+                        "--steps", "2", "--warmup", "1", "--corrupt-record", "7"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0, r.stdout[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["records_verified"] is False and out["parity_sample"]["mismatches"] == 1
+    assert "parity self-check failed" in r.stderr
+
+
+def test_parity_sample_counts_mismatches():
+    """bench.parity_sample on gathered record buffers: the sampled rows against the oracle, pads
+    skipped, one flipped end counted once, full=True checks every row."""
+    import sys
+    import numpy as np
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    import bench
+    import oracle_ffi as O
+    from svtrek_amd import sim
+    from svtrek_amd.distributed import padded_rows
+    r = sim.generate(sim.SimConfig(seed=31, n_targets=2, n_loci=300, del_frac=0.5, coverage=8.0))
+    want = O.refine_batch(r.pileup, r.loci)
+    per = padded_rows(len(r.loci), 2)
+    parts = []
+    for g in range(2):
+        rows = shard_rows(r.loci, 2, g)
+        parts.append(pack_records(rows, want[rows], per))
+    ps = bench.parity_sample(parts, r, np.arange(50), n_random=100, threads=2)
+    assert ps["mismatches"] == 0 and 100 <= ps["loci"] <= 150
+    assert bench.parity_sample(parts, r, [], full=True, threads=2)["loci"] == 300
+    parts[1][5, 2] ^= 1
+    ps = bench.parity_sample(parts, r, [], full=True, threads=2)
+    assert ps["mismatches"] == 1 and ps["first"]["vcf_row"] == int(parts[1][5, 0])
 
 
 def test_bench_refuses_world_size_mismatch():

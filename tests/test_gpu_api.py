@@ -191,3 +191,41 @@ def test_graph_replay_reindex(engine_factory):
 
 def test_locus_dtype_layout():
     assert LOCUS_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 16
+
+
+def test_graph_replays_between_direct_lane_launches(engine_factory):
+    """a captured lane launch replays with its capture's redo-counter parity
+    while direct launches in between flip it; the replay must leave both left-over counters zero,
+    or the next direct launch of the same parity appends after a stale count and re-runs windows
+    of the graph's batch.  Lane kernel forced, min_count 1 (left-overs in every launch); direct and
+    replayed launches alternate as direct, replay, direct, direct, replay, replay, direct."""
+    r = _workload(n_loci=4000, seed=72)
+    prm = Params(consensus_min_count=1)
+    eng = engine_factory(prm, gather="span")
+    eng.load_pileup(r.pileup)
+    want = O.refine_batch(r.pileup, r.loci, prm, threads=8)
+    n = len(r.loci)
+    small = r.loci[: n // 3]
+    want_small = want[: n // 3]
+    d_loci = torch.from_numpy(r.loci.view(np.uint8).copy()).cuda()
+    d_out = torch.zeros(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        eng.refine_device(d_loci.data_ptr(), n, d_out.data_ptr(), s.cuda_stream)
+
+    def replay():
+        d_out.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        _same(d_out.cpu().numpy().view(RESULT_DTYPE), want)
+
+    def direct():
+        _same(eng.refine(small), want_small)
+
+    for f in (direct, replay, direct, direct, replay, replay, direct):
+        f()

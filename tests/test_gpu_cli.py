@@ -127,3 +127,31 @@ def test_genomic_shards_on_one_device(tmp_path):
     want = O.audit_text(text, r.pileup)
     assert run_cli("-b", bam, "-v", str(vcf), "--devices", "0,0,0", "--batch", "50").stdout == want
     assert run_cli("-b", bam, "-v", str(vcf), "--devices", "0,0").stdout == want
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_audt_dist_two_ranks_engine(tmp_path):
+    """audt_dist with the real HIP engine in two rank processes (launched by
+    torch.distributed.run; on a one-GPU box both ranks share device 0 and the status all-reduce
+    and gather go through gloo): per-rank BAI region reads, the engine on each shard, the gather,
+    and stdout byte-identical to the oracle's for the whole VCF (audit.c:269-293)."""
+    import sys
+    r = sim.generate(sim.SimConfig(seed=52, n_targets=3, n_loci=400, del_frac=0.5, coverage=15), keep_handle=True)
+    bam = str(tmp_path / "d2.bam")
+    sim.write_bam(r, bam)
+    vcf = tmp_path / "d2.vcf"
+    sim.write_vcf(r.loci, str(vcf))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          "-m", "svtrek_amd.audt_dist", "-b", bam, "-v", str(vcf), "-t", "2"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600, cwd=ROOT, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = "".join(ln for ln in res.stdout.splitlines(keepends=True) if not ln.startswith("[Gloo]"))
+    assert out == O.audit_text(vcf.read_text(), r.pileup)

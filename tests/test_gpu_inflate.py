@@ -152,3 +152,34 @@ def test_inflate_incomplete_codes_as_zlib(engine_factory):
         else:
             with pytest.raises(RuntimeError, match="corrupt BGZF block 0"):
                 eng.bgzf_inflate(buf, blocks)
+
+
+def test_inflate_crafted_streams(engine_factory):
+    """the edge cases of the vector-side decoder -- matches 1921-2048 bytes back with
+    lengths 65-258 (the ring's far edge), every distance class, a stored block after a dynamic block
+    ending in a far match (and an empty stored block), outputs ending exactly on a 256-byte chunk,
+    literal/length and distance codes of 10-15 bits (past the 9-bit root) -- byte-identical to zlib,
+    in one batch at random alignments; and ISIZE off by one either way at a chunk boundary is
+    reported as zlib would (the stream does not inflate to its ISIZE)."""
+    rng = random.Random(23)
+    crafted = D.crafted_streams(random.Random(17))
+    for z, d, name in crafted:
+        assert zlib.decompressobj(-15).decompress(z) == d, name
+    streams = [(z, d) for z, d, _ in crafted] * 3
+    rng.shuffle(streams)
+    comp, blocks = _batch(streams, rng, out_skew=True)
+    eng = engine_factory()
+    got = eng.bgzf_inflate(comp, blocks)
+    for (z, d), b in zip(streams, blocks):
+        assert got[int(b["uoff"]):int(b["uoff"]) + len(d)].tobytes() == d, (len(z), len(d))
+    good = [(z, d) for z, d, name in crafted if name == "far_edge"]
+    for z, d, name in crafted:
+        if not name.startswith("chunk_end_"):
+            continue
+        for delta in (-1, 1):
+            if len(d) + delta > 65536:
+                continue
+            bad = (z, d[:-1] if delta < 0 else d + b"\0")
+            c2, b2 = _batch(good + [bad] + good, rng)
+            with pytest.raises(RuntimeError, match="corrupt BGZF block 1"):
+                eng.bgzf_inflate(c2, b2)
