@@ -185,6 +185,15 @@ def parity_sample(parts, res, first_rows, n_random: int = 10000, seed: int = 0, 
 
 STEP_KERNELS = ("ix2_census_kernel", "ix2_emit_kernel", "refine_lane_kernel", "refine_redo_kernel")
 STREAM_INDEX_KERNELS = ("index_kernel", "ix_copy_kernel")   # the long-read index build (svt_index.inc)
+BUCKET_INDEX_KERNELS = ("ixb_lane_kernel",)                  # the value buckets filed from the stream (short reads)
+BUCKET_STREAM_KERNELS = ("index_kernel", "ix_copy_kernel", "ixb_lists_kernel")   # ... from the span lists (long reads)
+
+
+def index_kernels(load_stats: dict) -> tuple:
+    """The kernels of one svt_reindex for this pileup (the step's index build)."""
+    if load_stats.get("bucket_index"):
+        return BUCKET_INDEX_KERNELS if load_stats.get("index_kind") == 1 else BUCKET_STREAM_KERNELS
+    return STEP_KERNELS[:2] if load_stats.get("index_kind") == 1 else STREAM_INDEX_KERNELS
 
 
 def _traffic(workload: str, records: bool) -> dict:
@@ -537,7 +546,7 @@ def main() -> int:
     value = total_loci / t_max
     ref_bytes = 24 * n + 12 * work["reads"] + 4 * work["ops_walked"]
     ev_bytes = int(work["event_bytes"]) + 12 * n   # records: 16-B result record (not 8) + 4-B row index
-    idx_bytes = int(load_stats.get("index_bytes", 0))
+    idx_bytes = int(load_stats.get("bucket_bytes" if load_stats.get("bucket_index") else "index_bytes", 0))
     alg_bytes = idx_bytes + ev_bytes               # the engine's algorithmic bytes of one step
     step_s = step_ms * 1e-3
     achieved = alg_bytes / step_s / 1e9
@@ -602,8 +611,7 @@ def main() -> int:
                              "def": "SURVEY 8(d): 24 B/locus + 12 B/yielded read + 4 B/CIGAR word the reference walk "
                                     "consumes (svt_count_work); the engine walks each read once, the reference once "
                                     "per window that yields it, so this is an effective rate, not DRAM traffic"},
-                         "kernel": "step = index build (" + ", ".join(STEP_KERNELS[:2] if load_stats.get("index_kind") == 1
-                                                                      else STREAM_INDEX_KERNELS) + ") + refine (" +
+                         "kernel": "step = index build (" + ", ".join(index_kernels(load_stats)) + ") + refine (" +
                                    (refine_kernel + (", refine_redo_kernel" if refine_kernel == "refine_lane_kernel"
                                                      else "")) + ")",
                          "step_ms_mean": round(step_ms, 5),
@@ -614,18 +622,29 @@ def main() -> int:
                              "index_ms": round(index_ms, 5), "refine_ms": round(refine_ms, 5),
                              "index_alg_bytes": idx_bytes,
                              "index_gbs": round(idx_bytes / (index_ms * 1e-3) / 1e9, 2) if idx_bytes else None,
-                             "index_bytes_def": "lane per read: CIGAR stream twice (4 B/op; census + emit), 65 B/read "
-                                                "(census soff, clip byte, counts; emit counts, soff, rec, offsets), 16 B/span "
-                                                "event; stream walk: the stream once, 56 B/read (soff, rec, staged and "
-                                                "placed offsets), 48 B/span event (staged, read back, placed) "
-                                                "(svt_load_stats.index_bytes)",
+                             "index_bytes_def": ("value buckets (svt_load_stats.bucket_bytes): short reads, the CIGAR "
+                                                 "stream once (4 B/op) + 24 B/read (offsets, record) + 28 B/filed event "
+                                                 "(16-B event written, its bucket's two 4-B offsets read, 4-B cursor "
+                                                 "incremented; a D > 50 op is filed twice); long reads, the span lists' "
+                                                 "build + 32 B/read + 16 B/list event read + 28 B/filed event"
+                                                 if load_stats.get("bucket_index") else
+                                                 "lane per read: CIGAR stream twice (4 B/op; census + emit), 65 B/read "
+                                                 "(census soff, clip byte, counts; emit counts, soff, rec, offsets), 16 B/span "
+                                                 "event; stream walk: the stream once, 56 B/read (soff, rec, staged and "
+                                                 "placed offsets), 48 B/span event (staged, read back, placed) "
+                                                 "(svt_load_stats.index_bytes)"),
                          },
                          "engine_bytes": {"bytes": ev_bytes, "ms": round(refine_ms, 5),
                                           "gbs": round(ev_bytes / (refine_ms * 1e-3) / 1e9, 2),
                                           "kernel": refine_kernel,
-                                          "def": "the refine launch alone, priced with the span walk's own bytes: "
-                                                 "36 B/locus + 32 B/query + 4 B/search entry + 16 B/span bounds + "
-                                                 "16 B/span event (svt_work)"}},
+                                          "def": ("the refine launch alone, priced with the value buckets' own bytes: "
+                                                  "36 B/locus (locus, 16-B record + 4-B row index) + 12 B/bucket query "
+                                                  "(two bucket offsets, one prefix-max key) + 16 B/event of the band's "
+                                                  "buckets and of the walks for ABOVE (svt_work)"
+                                                  if load_stats.get("bucket_index") else
+                                                  "the refine launch alone, priced with the span walk's own bytes: "
+                                                  "36 B/locus + 32 B/query + 4 B/search entry + 16 B/span bounds + "
+                                                  "16 B/span event (svt_work)")}},
             "index_build": {"index_ms_load": load_stats["index_ms"], "load_ms": load_stats,
                             "value_index_resident": round((n if args.emulate_shard else n_total) / (refine_ms * 1e-3), 1),
                             "note": "value_index_resident: loci/s of the refine launch alone, the index built once "

@@ -138,6 +138,13 @@ typedef struct svt_work {
     uint64_t event_bytes;    /* algorithmic bytes of the batch under the context's gather
                                 variant: 24 B per locus + its reads at their byte sizes
                                 (DESIGN.md "Roofline")                                    */
+    /* value-bucketed event index (the default since 0.24; zero with SVTREK_INDEX=lists) */
+    uint64_t bucket_queries; /* windows answered from the value buckets: two 4-B bucket
+                                offsets + one 4-B prefix-max key each                      */
+    uint64_t bucket_events;  /* 16-B events of the band's buckets, plus those of the
+                                bounded walks for the facts above the band when the vote
+                                needs them (event_bytes prices these instead of the span
+                                walk's when the bucket index is on)                       */
 } svt_work;
 
 /* One refined call as the multi-GPU gather moves it: the record's index
@@ -286,6 +293,18 @@ typedef struct svt_load_stats {
     uint64_t lead_blocks;   /* always 0 (the lead chunks of rounds 1-3 are gone since 0.17)      */
     uint64_t slow_reads;    /* reads whose walk reaches 2^28 bases or position 2^29              */
     uint64_t index_kind;    /* the index build used: 1 lane per read, 2 stream walk              */
+    /* the value-bucketed event index (0.24, DESIGN.md "Value buckets"): every candidate event
+     * filed by its candidate value in 1 kb buckets, per window kind -- the refine kernels read a
+     * window's band from it, svt_reindex rebuilds it (and, with long reads, the span lists it is
+     * filed from).  0 everywhere with SVTREK_INDEX=lists (the span lists alone, rounds 1-5). */
+    uint64_t bucket_index;  /* 1: on                                                              */
+    uint64_t buckets;       /* buckets per event array (every contig's, incl. its overflow bucket) */
+    uint64_t bucket_events; /* events filed per rebuild (a D > 50 op twice: by start and by end)   */
+    uint64_t bucket_bytes;  /* algorithmic bytes of one rebuild: lane per read, the CIGAR stream
+                               once (4 B/op) + 24 B per read (offsets, record) + 28 B per filed
+                               event (16-B event written, its bucket's two 4-B offsets read and
+                               4-B cursor incremented); long reads: the span-list build's bytes +
+                               16 B per list event read + 28 B per filed event                    */
 } svt_load_stats;
 svt_status svt_last_load_stats(const svt_ctx *ctx, svt_load_stats *out);
 

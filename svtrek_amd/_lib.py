@@ -85,6 +85,8 @@ class SvtWork(C.Structure):
         ("span_bounds", C.c_uint64),
         ("span_events", C.c_uint64),
         ("event_bytes", C.c_uint64),
+        ("bucket_queries", C.c_uint64),
+        ("bucket_events", C.c_uint64),
     ]
 
 
@@ -99,6 +101,10 @@ class SvtLoadStats(C.Structure):
         ("lead_blocks", C.c_uint64),
         ("slow_reads", C.c_uint64),
         ("index_kind", C.c_uint64),
+        ("bucket_index", C.c_uint64),
+        ("buckets", C.c_uint64),
+        ("bucket_events", C.c_uint64),
+        ("bucket_bytes", C.c_uint64),
     ]
 
 

@@ -41,7 +41,8 @@ def build_engine(force: bool = False) -> str:
     out = os.path.join(PKG, "libsvtrek_hip.so")
     deps = [os.path.join(CSRC, "svt_engine.hip"), os.path.join(INC, "svtrek_gpu.h"), os.path.join(CSRC, "svt_poa.inc"),
             os.path.join(CSRC, "svt_index.inc"), os.path.join(CSRC, "svt_index2.inc"),
-            os.path.join(CSRC, "svt_inflate.inc"), os.path.join(CSRC, "svt_bamrec.h"), os.path.join(CSRC, "svt_bam.inc")]
+            os.path.join(CSRC, "svt_inflate.inc"), os.path.join(CSRC, "svt_bamrec.h"), os.path.join(CSRC, "svt_bam.inc"),
+            os.path.join(CSRC, "svt_bucket.inc"), os.path.join(CSRC, "svt_bucket_build.inc")]
     if force or _stale(out, deps):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
               "-Wall", "-I", INC, "-o", out, deps[0]])
@@ -54,7 +55,8 @@ def build_test_engine(force: bool = False) -> str:
     out = os.path.join(PKG, "variants", "libsvtrek_hip_ring2.so")
     deps = [os.path.join(CSRC, "svt_engine.hip"), os.path.join(INC, "svtrek_gpu.h"), os.path.join(CSRC, "svt_poa.inc"),
             os.path.join(CSRC, "svt_index.inc"), os.path.join(CSRC, "svt_index2.inc"),
-            os.path.join(CSRC, "svt_inflate.inc"), os.path.join(CSRC, "svt_bamrec.h"), os.path.join(CSRC, "svt_bam.inc")]
+            os.path.join(CSRC, "svt_inflate.inc"), os.path.join(CSRC, "svt_bamrec.h"), os.path.join(CSRC, "svt_bam.inc"),
+            os.path.join(CSRC, "svt_bucket.inc"), os.path.join(CSRC, "svt_bucket_build.inc")]
     if force or _stale(out, deps):
         os.makedirs(os.path.dirname(out), exist_ok=True)
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DSVT_POA_RING=2",

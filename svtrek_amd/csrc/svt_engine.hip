@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.23.4 (gfx950, index build by read length / one-pass stream walk with light slots at 7 waves/SIMD, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.24.0 (gfx950, value-bucketed event index filed by a lane-per-read walk, band + prefix-max facts, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -86,6 +86,23 @@ struct DevPileup {
     int32_t n_targets;
 };
 
+// The value-bucketed event index (svt_bucket.inc, svt_bucket_build.inc): per window kind one array
+// of events filed by candidate value in 1 kb buckets per contig.
+constexpr int BKS = 10;                                  // bucket = 1 kb of candidate value
+constexpr int BA_S = 0, BA_E = 1, BA_I = 2, BA_L = 3, BA_N = 4;
+struct BkIndex {
+    const uint4 *ev;              // the events of the four arrays, S, E, I, L one after the other -- S: D > 50
+                                  // + trailing S by x; E: D > 50 by x + len + 1, leading S by walk end + 1;
+                                  // I: I >= 50 by x; L: leading S by read start
+    const uint32_t *off;          // [BA_N][nbk + 1] first event (an index into ev) of every bucket
+    const int32_t *pm;            // [3][nbk + 1] S, E, I: prefix max (within the contig) of the BELOW keys
+    const uint64_t *cbase;        // [n_targets] contig t's first bucket
+    const uint32_t *cnb;          // [n_targets] its buckets (the last one: every value past the others)
+    const uint32_t *maxd;         // [n_targets] its longest D > 50 op (0: none)
+    uint64_t nbk;                 // buckets per array (every contig's)
+    int on;                       // built (SVTREK_INDEX=lists: 0, the span lists alone)
+};
+
 struct KParams {
     int32_t wider, median, narrow, range, ci, min_count;
     int32_t sw_window, sw_slide;   // sliding_window_ins mode only
@@ -117,12 +134,13 @@ struct KArgs {
     uint32_t *redo_list;        // lane-vote launches: windows left for refine_redo_kernel
     uint32_t *redo_ctr;         //   their count (this launch's counter)
     uint32_t *redo_next;        //   the next launch's counter (reset by refine_redo_kernel)
+    BkIndex bk;                 // the value-bucketed event index
 };
 
 // svt_work counter slots (refine_window's wk[], the context's work words)
 constexpr int W_WINDOWS = 0, W_READS = 1, W_OPS = 2, W_CANDS = 3, W_SPILLED = 4, W_QUERIES = 5, W_PROBE = 6,
               W_RANGE = 7, W_LREADS = 8, W_LENTRIES = 9, W_STOPS = 10, W_STOPCH = 11, W_SQUERIES = 12,
-              W_SPAN = 13, W_N = 14;
+              W_SPAN = 13, W_BQ = 14, W_BEV = 15, W_N = 16;
 constexpr size_t CTL_BYTES = 256;   // context control words: pool head, status, work counters
 constexpr size_t CTL_REDO = 200;    // redo counters: two alternating (direct launches), one + scratch (captured)
 static_assert(16 + 8 * W_N <= CTL_REDO && CTL_REDO + 16 <= CTL_BYTES, "control block too small");
@@ -1034,6 +1052,10 @@ __device__ __forceinline__ int32_t vote_window(const KArgs &a, WinLds &lds, int 
     return sort_and_vote<VOTE, true>(g, gp, n, (int32_t)imprecise, a.prm, support);
 }
 
+constexpr int LV_WMAX = 1023;   // band half-width for 16-bit offsets and prefix sums (32 * 2046 < 2^16)
+
+#include "svt_bucket.inc"
+
 // One wave per query window, WPB independent waves per workgroup.  Window g < n is locus
 // g's first window (DEL: refine_start over [pos-wider, pos+narrow], INS: refine_ins),
 // window n + i is locus i's second (DEL: refine_end over end +- narrow): the wide windows
@@ -1110,7 +1132,9 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
         else { kind = K_END; s = end - (uint32_t)k.narrow; e = end + (uint32_t)k.narrow; imp = end; }
     }
     uint32_t r = SVT_NA;
-    if (kind >= 0) {
+    // the value buckets first (svt_bucket.inc); the span lists for the windows they do not take
+    const bool bk_done = !COUNT && kind >= 0 && refine_any_bk<false>(a, lds, kind, chrom, s, e, imp, wk, r);
+    if (kind >= 0 && !bk_done) {
         // the kind-specific gathers, then ONE copy of the sort + vote for all kinds (code size:
         // the three inlined copies of the vote no longer compete for the instruction cache)
         int32_t n;
@@ -1125,6 +1149,11 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
         else if (kind == K_INS) r = (uint32_t)vote_window<K_INS, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
         else if (kind == K_START) r = (uint32_t)vote_window<K_START, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
         else r = (uint32_t)vote_window<K_END, COUNT, G, V_CONSENSUS>(a, lds, chrom, s, e, imp, n, wk, sup);
+        if (COUNT) {   // what the bucket path reads for this window (its result is the same)
+            wave_sync();
+            uint32_t rb = 0;
+            (void)refine_any_bk<true>(a, lds, kind, chrom, s, e, imp, wk, rb);
+        }
     }
     if (lane_id() == 0) {
         write_result(a, li, w, r);
@@ -1152,7 +1181,6 @@ __device__ __forceinline__ void refine_body(const KArgs &a) {
 constexpr int LV_CAP = 32;   // band elements a lane votes on
 constexpr int LV_S = 34;     // u16 per staged row (17 words: odd -> no bank conflicts)
 static_assert(LV_S > LV_CAP, "a staged row needs a spare slot past LV_CAP");
-constexpr int LV_WMAX = 1023;   // band half-width for 16-bit offsets and prefix sums (32 * 2046 < 2^16)
 // LV_BELOW / LV_ABOVE: some candidate lies at or below the band's low end / at or above its high
 // end (with the band itself they give band_filter's whole-multiset facts, see lane_vote)
 constexpr uint32_t LV_PENDING = 1u << 8, LV_BELOW = 1u << 9, LV_ABOVE = 1u << 10,
@@ -1181,7 +1209,7 @@ struct alignas(16) LvWin {
     int32_t lo;     // the band's low end
     uint32_t kl;    // kind | the window's lane (row) << 8
     uint32_t len;   // span events (> 0)
-    uint32_t pad;
+    uint32_t pad;   // value buckets: LV_BELOW when the prefix maxima below the band's buckets hold a candidate
 };
 
 template <int W>
@@ -1233,18 +1261,30 @@ struct LwWin {
     int32_t lo1;    // lo + 1: a value v is at or below the band when v - lo1 < 0
     int32_t hm1;    // hi - 1: at or above it when hm1 - v < 0
     uint32_t wb;    // hi - lo - 1: in the band when (uint32)(v - lo1) < wb
+    int32_t em2;    // e - 2 (value buckets: the event's read is yielded when its pos <= e - 2)
 };
 __device__ __forceinline__ uint32_t sgn(int32_t d) { return (uint32_t)d >> 31; }
 __device__ __forceinline__ uint32_t opbit(uint32_t set, uint32_t op) { return __builtin_amdgcn_ubfe(set, op, 1); }
 
 // One 64-event slot: the band's lane mask; below / above accumulated into the sign bits of
 // belv / abv; iv = the lane's candidate value.
-template <int KIND>
+template <int KIND, bool BK>
 __device__ __forceinline__ uint64_t slot_vl(const uint4 &v, const LwWin &W, uint32_t &belv, uint32_t &abv, int32_t &iv) {
     const uint32_t op = v.y & 0xfu;
-    const uint32_t far = sgn((int32_t)v.z - W.b1) | sgn((int32_t)W.e - (int32_t)v.x);   // no overlap / not reached
+    // value buckets: the event's read must also be yielded (its pos -- v.w, v.x for a leading S --
+    // below the query end); a span holds only yielded reads' events
+    const uint32_t yld = BK ? sgn(W.em2 - (int32_t)v.w) : 0u;
+    const uint32_t far = sgn((int32_t)v.z - W.b1) | sgn((int32_t)W.e - (int32_t)v.x) | yld;   // no overlap / not reached
     uint32_t fail;
-    if (KIND == K_INS) {                                                  // refinement.c:299
+    if (BK && KIND == K_END) {                                            // :188, :210-220
+        const uint32_t isD = opbit(1u << OP_DEL, op), isL = opbit(1u << SP_LEAD, op);
+        const uint32_t lead = isL & (sgn((int32_t)v.z - W.b1) ^ 1u) & (sgn((int32_t)v.x - W.sc) ^ 1u) &
+                              (sgn(W.em2 - (int32_t)v.x) ^ 1u);
+        const uint32_t brk = lead & sgn((int32_t)W.e - (int32_t)v.w);   // walk passes e: a value >= e + 2
+        abv |= brk << 31;
+        fail = ((isD & (far ^ 1u)) | (lead & (brk ^ 1u))) ^ 1u;
+        iv = (int32_t)(isD ? v.x + (v.y >> 4) + 1u : v.w + 1u);
+    } else if (KIND == K_INS) {                                           // refinement.c:299
         fail = far | (opbit(1u << OP_INS, op) ^ 1u);
         iv = (int32_t)v.x;
     } else if (KIND == K_START) {                                         // :124, :147
@@ -1270,7 +1310,7 @@ __device__ __forceinline__ uint64_t slot_vl(const uint4 &v, const LwWin &W, uint
 // row) come from the caller's v_readlane of per-lane values computed once per wave.  Every lane
 // stores in every slot -- members to their row slot, the others to their own sink word -- so a
 // slot costs no exec-mask round trip on the scalar unit.
-template <int KIND>
+template <int KIND, bool BK>
 __device__ __forceinline__ LaneBand lane_walk(uint64_t evaddr, uint32_t len, const LwWin &W, int32_t lo, uint16_t *row,
                                               uint16_t *sink) {
     const int ln = lane_id();
@@ -1290,7 +1330,7 @@ __device__ __forceinline__ LaneBand lane_walk(uint64_t evaddr, uint32_t len, con
         for (int u = 0; u < LW_U; u++) {
             if ((uint32_t)(u * WAVE) >= left) break;
             int32_t iv;
-            const uint64_t mb = slot_vl<KIND>(v[u], W, belv, abv, iv);
+            const uint64_t mb = slot_vl<KIND, BK>(v[u], W, belv, abv, iv);
             // members past LV_CAP all land in the row's spare slot LV_CAP (the window is redone);
             // the slot is computed by every lane (the empty asm keeps the compiler from moving it
             // under a branch on the member mask), then one select
@@ -1315,7 +1355,7 @@ struct LwOne {
     int32_t lo;
     uint16_t *row;
 };
-template <int KIND>
+template <int KIND, bool BK>
 __device__ __forceinline__ void lane_walk2(const LwOne &A, const LwOne &B, uint16_t *sink, LaneBand &ra, LaneBand &rb) {
     const int ln = lane_id();
     const __amdgpu_buffer_rsrc_t sa = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A.base), (short)0,
@@ -1341,7 +1381,7 @@ __device__ __forceinline__ void lane_walk2(const LwOne &A, const LwOne &B, uint1
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             int32_t iv;
-            const uint64_t mb = slot_vl<KIND>(v[2 * w + u], O.W, belv, abv, iv);
+            const uint64_t mb = slot_vl<KIND, BK>(v[2 * w + u], O.W, belv, abv, iv);
             uint32_t at = (uint32_t)min(nb + (int32_t)mbcnt(mb), LV_CAP);
             asm volatile("" : "+v"(at));
             uint16_t *dst = __builtin_amdgcn_inverse_ballot_w64(mb) ? O.row + at : sink;
@@ -1359,21 +1399,25 @@ __device__ __forceinline__ void lane_walk2(const LwOne &A, const LwOne &B, uint1
 // s / e / band (the tests of span_cand_mask, per lane); members go to the window's row at
 // their rank among its members, and each window's first lane writes its meta row (band size,
 // candidates, below / above) -- everything lane_walk gives a window, for 1-64 events at once.
-__device__ __forceinline__ void lane_packed(const DevPileup &P, const LvWin *win, LvMeta *meta, uint16_t *stage,
-                                            uint32_t c0, uint64_t M, uint32_t tot, int32_t bw2) {
+template <bool BK>
+__device__ __forceinline__ void lane_packed(const DevPileup &P, const BkIndex &B, const LvWin *win, LvMeta *meta,
+                                            uint16_t *stage, uint32_t c0, uint64_t M, uint32_t tot, int32_t bw2) {
     const int ln = lane_id();
     const uint64_t upto = M & ((2ull << ln) - 1ull);   // marks at or below this lane (ln 63: all)
     const uint32_t r = (uint32_t)__popcll(upto) - 1u, f = 63u - (uint32_t)__clzll(upto);
     const LvWin w = win[c0 + r];
     const uint32_t kind = w.kl & 0xffu, k = w.kl >> 8;
-    const uint4 *evb = (kind == (uint32_t)K_INS ? P.spI : P.spD) + w.e0;
+    const uint4 *evb = (BK ? B.ev : kind == (uint32_t)K_INS ? P.spI : P.spD) + w.e0;
     const uint4 v = evb[min((uint32_t)ln - f, w.len - 1u)];   // lanes past tot: their window's last event
     const uint32_t s = w.s, e = w.e, x = v.x, op = v.y & 0xfu;
     const int32_t lo = w.lo;
-    const uint64_t base = ballot((uint32_t)ln < tot) & ballot((int32_t)v.z > (int32_t)(s - 1u)) & ballot(x <= e);
     const uint64_t isI = ballot(kind == (uint32_t)K_INS), isE = ballot(kind == (uint32_t)K_END);
-    const uint64_t oD = ballot(op == OP_DEL), sx = ballot(s <= x);
-    const uint64_t lead = base & isE & ballot(op == SP_LEAD) & sx;   // refinement.c:210-220
+    const uint64_t oD = ballot(op == OP_DEL), sx = ballot(s <= x), oL = ballot(op == SP_LEAD);
+    const uint64_t ovl = ballot((int32_t)v.z > (int32_t)(s - 1u));
+    // value buckets: the event's read is yielded (pos < e - 1: v.w, or v.x for a leading S)
+    const uint64_t yw = BK ? ballot(v.w + 2u <= e) : ~0ull, yx = BK ? ballot(x + 2u <= e) : ~0ull;
+    const uint64_t base = ballot((uint32_t)ln < tot) & ovl & ballot(x <= e) & (yw | (isE & oL));
+    const uint64_t lead = ballot((uint32_t)ln < tot) & ovl & isE & oL & sx & (BK ? yx : ballot(x <= e));   // :210-220
     const uint64_t brk = lead & ballot(v.w > e);
     const uint64_t cm = (base & ((isI & ballot(op == OP_INS)) | (~(isI | isE) & (oD | (ballot(op == SP_TRAIL) & sx))) |
                                  (isE & oD))) |
@@ -1390,7 +1434,7 @@ __device__ __forceinline__ void lane_packed(const DevPileup &P, const LvWin *win
         const uint32_t nb = (uint32_t)__popcll(mb & rm);
         const bool below = (cm & ~gt & rm) != 0ull, above = ((brk | (cm & ~lt)) & rm) != 0ull;
         meta[k].flags = nb > (uint32_t)LV_CAP ? (LV_REDO | LV_WHY(3))
-                                              : nb | LV_PENDING | (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u);
+                                              : nb | LV_PENDING | (below ? LV_BELOW : 0u) | (above ? LV_ABOVE : 0u) | w.pad;
         meta[k].n = 0;
     }
 }
@@ -1526,6 +1570,7 @@ struct LvQuery {
     int32_t lo;            // the vote's band low end: pos - (range + max(ci, 0))
     uint32_t s, e, liw, len;        // the window, li << 1 | w, its span's event count
     uint32_t e0[2];                 // the span's first event
+    uint32_t fl;                    // value buckets: LV_BELOW from the prefix maxima
 };
 static_assert(sizeof(LvQuery) <= LV_S * 2, "LvQuery must fit a staging row");
 
@@ -1582,6 +1627,38 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
     q.len = (uint32_t)(E1 - E0);
 }
 
+// lane_query for the value buckets (svt_bucket.inc): A2, the window's eligibility, its band's bucket
+// span and the prefix maxima's BELOW -- no region query, no binary search (one dependent step after
+// the locus: the contig's bucket base, then the two bucket offsets and one prefix-max key).
+__device__ __forceinline__ void lane_query_bk(const KArgs &a, uint32_t g, LvQuery &q) {
+    const KParams &k = a.prm;
+    const uint32_t w = g >= a.n ? 1u : 0u, li = g - w * a.n;
+    const svt_locus L = a.loci[li];
+    q.kind = -1;
+    q.liw = li << 1 | w;
+    q.len = 0;
+    q.fl = 0;
+    const uint32_t pos = L.pos, end = L.end;
+    uint32_t imp = 0;
+    if (L.type == T_INS && w == 0) { q.kind = K_INS; q.s = pos - (uint32_t)k.median; q.e = pos + (uint32_t)k.median; imp = pos; }
+    else if (L.type == T_DEL && w == 0) { q.kind = K_START; q.s = pos - (uint32_t)k.wider; q.e = pos + (uint32_t)k.narrow; imp = pos; }
+    else if (L.type == T_DEL) { q.kind = K_END; q.s = end - (uint32_t)k.narrow; q.e = end + (uint32_t)k.narrow; imp = end; }
+    if (q.kind < 0) return;   // INV: refine_point collects only when sv_type == SV_INS (refinement.c:250): NA, NA
+    BkWin W;
+    const int el = bk_eligible(a, q.kind, L.chrom, q.s, q.e, imp, W);
+    if (el == 0) { q.kind |= LQ_REDO; return; }   // the span-list path (refine_redo_kernel)
+    q.lo = (int32_t)imp - (k.range + max(k.ci, 0));
+    if (el < 0) return;                            // A3: no reads -> nb = 0 -> NA
+    uint32_t E0, E1;
+    bool below;
+    bk_query(a.bk, q.kind, L.chrom - 1, W, E0, E1, below);
+    if (E1 - E0 >= LW_BUF_MAX) { q.kind |= LQ_REDO; return; }   // (lane_walk's buffer byte count)
+    q.e0[0] = E0;
+    q.e0[1] = 0u;
+    q.len = E1 - E0;
+    q.fl = below ? LV_BELOW : 0u;
+}
+
 // SVT_PHASE_PROF (diagnostic builds): every wave of refine_lane_kernel adds its phases' wall
 // time (100 MHz ticks) and work counts into ph_prof, read (and cleared) by svt_diag_phase.
 #ifndef SVT_PHASE_PROF
@@ -1591,7 +1668,7 @@ __device__ __forceinline__ void lane_query(const KArgs &a, uint32_t g, bool band
 __device__ unsigned long long ph_prof[16];
 #define PH_ADD(i, v) atomicAdd(&ph_prof[i], (unsigned long long)(v))
 #endif
-template <int LV_W>
+template <int LV_W, bool BK>
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) {
     __shared__ LaneLds<LV_W> lds_all[WPB];
     const uint32_t wid = threadIdx.x >> 6;
@@ -1615,7 +1692,10 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     {
         const bool mine = (uint32_t)ln < cnt;
         LvQuery q{};
-        if (mine) lane_query(a, g0 + (uint32_t)ln, band_ok, q);
+        if (mine) {
+            if (BK) lane_query_bk(a, g0 + (uint32_t)ln, q);
+            else lane_query(a, g0 + (uint32_t)ln, band_ok, q);
+        }
         const bool walk = mine && q.kind >= 0 && !(q.kind & LQ_REDO) && q.len != 0u;
         if (mine) {
             uint32_t *row32 = reinterpret_cast<uint32_t *>(L.stage + (uint32_t)ln * LV_S);
@@ -1637,7 +1717,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             wn.lo = q.lo;
             wn.kl = (uint32_t)q.kind | (uint32_t)ln << 8;
             wn.len = q.len;
-            wn.pad = 0u;
+            wn.pad = q.fl;
             L.win[mbcnt(wm)] = wn;
         }
         nwin = (uint32_t)__popcll(wm);
@@ -1663,12 +1743,14 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     {
         const bool has = (uint32_t)ln < nwin;
         const LvWin wv = L.win[has ? (uint32_t)ln : 0u];   // (entry 0 unused when nwin == 0)
-        const uint32_t lenv = has ? wv.len : 0u, klv = wv.kl, ev = wv.e;
+        const uint32_t lenv = has ? wv.len : 0u, klv = wv.kl, ev = wv.e, flv = wv.pad;
+        const int32_t em2v = (int32_t)(wv.e - 2u);
         const int32_t lov = wv.lo;
         const int32_t b1v = max((int32_t)(wv.s - 1u), -(1 << 30)) + 1;
         const int32_t scv = (int32_t)min(wv.s, 0x7fffffffu);
-        const uint64_t addrv =
-            reinterpret_cast<uint64_t>(((klv & 0xffu) == (uint32_t)K_INS ? a.pile.spI : a.pile.spD) + wv.e0);
+        const uint64_t addrv = reinterpret_cast<uint64_t>(
+            (BK ? a.bk.ev : (klv & 0xffu) == (uint32_t)K_INS ? a.pile.spI : a.pile.spD) +
+            wv.e0);
         uint16_t *sink = reinterpret_cast<uint16_t *>(&L.sink[ln]);
         const int32_t bw2 = 2 * bw;
 #if SVT_PHASE_PROF
@@ -1692,16 +1774,18 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                         const int32_t lo = rdlane_i(lov, (int)cc);
                         return LwOne{rdlane64(addrv, (int)cc), len,
                                      LwWin{rdlane_i(b1v, (int)cc), rdlane(ev, (int)cc), rdlane_i(scv, (int)cc), lo + 1,
-                                           lo + bw2 - 1, (uint32_t)(bw2 - 1)},
+                                           lo + bw2 - 1, (uint32_t)(bw2 - 1), rdlane_i(em2v, (int)cc)},
                                      lo, L.stage + (kl >> 8) * LV_S};
                     };
                     const LwOne A = one(c, ka, l0), B = one(c + 1u, kb, l1);
                     LaneBand ra, rb;
-                    if ((ka & 0xffu) == (uint32_t)K_INS) lane_walk2<K_INS>(A, B, sink, ra, rb);
-                    else if ((ka & 0xffu) == (uint32_t)K_START) lane_walk2<K_START>(A, B, sink, ra, rb);
-                    else lane_walk2<K_END>(A, B, sink, ra, rb);
-                    const uint32_t fa = ra.nb > LV_CAP ? (LV_REDO | LV_WHY(3)) : (uint32_t)ra.nb | LV_PENDING | ra.flags;
-                    const uint32_t fb = rb.nb > LV_CAP ? (LV_REDO | LV_WHY(3)) : (uint32_t)rb.nb | LV_PENDING | rb.flags;
+                    if ((ka & 0xffu) == (uint32_t)K_INS) lane_walk2<K_INS, BK>(A, B, sink, ra, rb);
+                    else if ((ka & 0xffu) == (uint32_t)K_START) lane_walk2<K_START, BK>(A, B, sink, ra, rb);
+                    else lane_walk2<K_END, BK>(A, B, sink, ra, rb);
+                    const uint32_t fa = ra.nb > LV_CAP ? (LV_REDO | LV_WHY(3))
+                                                       : (uint32_t)ra.nb | LV_PENDING | ra.flags | rdlane(flv, (int)c);
+                    const uint32_t fb = rb.nb > LV_CAP ? (LV_REDO | LV_WHY(3))
+                                                       : (uint32_t)rb.nb | LV_PENDING | rb.flags | rdlane(flv, (int)(c + 1u));
                     aflags = (uint32_t)ln == (ka >> 8) ? fa : (uint32_t)ln == (kb >> 8) ? fb : aflags;
                     c += 2u;
                     continue;
@@ -1711,14 +1795,14 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 const uint32_t kl = rdlane(klv, (int)c), kind = kl & 0xffu, kw = kl >> 8;
                 const int32_t lo = rdlane_i(lov, (int)c);
                 const LwWin W{rdlane_i(b1v, (int)c), rdlane(ev, (int)c), rdlane_i(scv, (int)c), lo + 1, lo + bw2 - 1,
-                              (uint32_t)(bw2 - 1)};
+                              (uint32_t)(bw2 - 1), rdlane_i(em2v, (int)c)};
                 const uint64_t base = rdlane64(addrv, (int)c);
                 uint16_t *row = L.stage + kw * LV_S;
                 LaneBand r;
-                if (kind == (uint32_t)K_INS) r = lane_walk<K_INS>(base, l0, W, lo, row, sink);
-                else if (kind == (uint32_t)K_START) r = lane_walk<K_START>(base, l0, W, lo, row, sink);
-                else r = lane_walk<K_END>(base, l0, W, lo, row, sink);
-                const uint32_t f = r.nb > LV_CAP ? (LV_REDO | LV_WHY(3)) : (uint32_t)r.nb | LV_PENDING | r.flags;
+                if (kind == (uint32_t)K_INS) r = lane_walk<K_INS, BK>(base, l0, W, lo, row, sink);
+                else if (kind == (uint32_t)K_START) r = lane_walk<K_START, BK>(base, l0, W, lo, row, sink);
+                else r = lane_walk<K_END, BK>(base, l0, W, lo, row, sink);
+                const uint32_t f = r.nb > LV_CAP ? (LV_REDO | LV_WHY(3)) : (uint32_t)r.nb | LV_PENDING | r.flags | rdlane(flv, (int)c);
                 aflags = (uint32_t)ln == kw ? f : aflags;
                 c++;
                 continue;
@@ -1731,7 +1815,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 M |= 1ull << tot;
                 tot += l;
             }
-            lane_packed(a.pile, L.win, L.meta, L.stage, c, M, tot, bw2);
+            lane_packed<BK>(a.pile, a.bk, L.win, L.meta, L.stage, c, M, tot, bw2);
             c = c1;
         }
         wave_sync();
@@ -1783,7 +1867,13 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             else if (nmax <= 16) lv_oe_sort<0, 16>(x);
             else lv_oe_sort<0, 32>(x);
             uint32_t *wrow = reinterpret_cast<uint32_t *>(row);
-            if (pend) {
+            // value buckets: ABOVE was only seen as far as the band's buckets; the vote reads it
+            // only when no candidate lies below pos - 25 (lane_vote's q) -- then the wave-wide path
+            // walks for it (bk_above, refine_redo_kernel)
+            const bool needA = BK && pend && !(mt.flags & (LV_BELOW | LV_ABOVE)) &&
+                               (int32_t)x[0] >= bw - SV_MIN_LENGTH / 2;
+            redo |= ballot(needA);
+            if (pend && !needA) {
 #pragma unroll
                 for (int j = 0; j < LV_CAP; j += 2) wrow[j >> 1] = x[j] | x[j + 1] << 16;
                 // the band elements <= pos + 25, counted on the sorted registers (no search)
@@ -1843,7 +1933,8 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_redo_kernel(KArgs a) 
         unsigned long long wk[W_N];
         int32_t sup;
         uint32_t r = SVT_NA;
-        if (kind == K_INS) r = (uint32_t)refine_window<K_INS, false, G_SPAN>(a, lds, chrom, s, e, imp, wk, sup);
+        if (kind >= 0 && refine_any_bk<false>(a, lds, kind, chrom, s, e, imp, wk, r)) {}   // the value buckets
+        else if (kind == K_INS) r = (uint32_t)refine_window<K_INS, false, G_SPAN>(a, lds, chrom, s, e, imp, wk, sup);
         else if (kind == K_START) r = (uint32_t)refine_window<K_START, false, G_SPAN>(a, lds, chrom, s, e, imp, wk, sup);
         else if (kind == K_END) r = (uint32_t)refine_window<K_END, false, G_SPAN>(a, lds, chrom, s, e, imp, wk, sup);
         if (lane_id() == 0) write_result(a, li, w, r);
@@ -1884,6 +1975,7 @@ __global__ void sw_reduce_kernel(const int2 *sub, const uint64_t *off, uint32_t 
 
 #include "svt_index.inc"
 #include "svt_index2.inc"
+#include "svt_bucket_build.inc"
 #include "svt_poa.inc"
 #include "svt_bam.inc"
 
@@ -1940,6 +2032,20 @@ struct svt_ctx {
     uint64_t poa_deferred = 0;        // loci the last svt_poa_consensus reran on full-size slots
     uint64_t *d_spoffD = nullptr, *d_spoffI = nullptr;   // span walk
     uint4 *d_spD = nullptr, *d_spI = nullptr;
+    // the value-bucketed event index (svt_bucket.inc, svt_bucket_build.inc)
+    bool bk_on = true;                // SVTREK_INDEX=lists: off (the span lists alone, rounds 1-5)
+    bool bk_ready = false;            // built for the loaded pileup
+    uint64_t bk_n = 0;                // buckets per array (every contig's)
+    uint32_t *d_bkoff = nullptr;      // [BA_N][bk_n + 1] extents (indices into d_bkev)
+    uint32_t *d_bkcur = nullptr;      // [BA_N][bk_n + 1] cursors of direct builds (k * count before build k)
+    uint32_t *d_bkcap = nullptr;      // [BA_N][bk_n + 1] cursors of captured builds (zeroed by the graph)
+    int32_t *d_bkpm = nullptr;        // [3][bk_n + 1] prefix max of the BELOW keys
+    uint4 *d_bkev = nullptr;          // every array's events
+    uint64_t bk_events[BA_N] = {};
+    uint64_t *d_bkbase = nullptr;     // [n_targets] first bucket of contig t
+    uint32_t *d_bknb = nullptr;       // [n_targets] its buckets
+    uint32_t *d_bkmaxd = nullptr;     // [n_targets] its longest D > 50 op
+    uint32_t bk_builds = 0;           // filing passes so far (the cursors' epoch)
     uint64_t dev_bytes = 0;
     bool loaded = false;
     svt_load_stats load_stats{};      // timings of the last svt_load_pileup
@@ -2043,6 +2149,10 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_part); hfree(c->d_cnt); hfree(c->d_agg); hfree(c->d_bsum); hfree(c->d_bpre); hfree(c->d_tot);
     hfree(c->d_scr); hfree(c->d_scrh); hfree(c->d_ovf);
     hfree(c->d_spoffD); hfree(c->d_spoffI); hfree(c->d_spD); hfree(c->d_spI);
+    hfree(c->d_bkoff); hfree(c->d_bkcur); hfree(c->d_bkcap); hfree(c->d_bkev); hfree(c->d_bkpm);
+    for (int A = 0; A < BA_N; A++) c->bk_events[A] = 0;
+    hfree(c->d_bkbase); hfree(c->d_bknb); hfree(c->d_bkmaxd);
+    c->bk_ready = false; c->bk_n = 0; c->bk_builds = 0;
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
     c->n_evD = c->n_evI = 0;
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
@@ -2074,6 +2184,14 @@ KArgs make_args(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, uint32_t
     a.rec_base = 0;
     a.redo_list = nullptr;
     a.redo_ctr = a.redo_next = nullptr;
+    a.bk.ev = c->d_bkev;
+    a.bk.off = c->d_bkoff;
+    a.bk.pm = c->d_bkpm;
+    a.bk.nbk = c->bk_n;
+    a.bk.cbase = c->d_bkbase;
+    a.bk.cnb = c->d_bknb;
+    a.bk.maxd = c->d_bkmaxd;
+    a.bk.on = c->bk_ready ? 1 : 0;
     return a;
 }
 
@@ -2135,8 +2253,9 @@ svt_status launch(svt_ctx *c, const svt_locus *d_loci, svt_result *d_out, size_t
         }
         // (16 windows a wave for the 250K-window launches of a 125K-locus shard measured slower:
         // 0.132-0.138 vs 0.117-0.121 ms, profiles/r04_sh)
-        hipLaunchKernelGGL(refine_lane_kernel<32>, dim3((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32))), block, 0,
-                           st, a);
+        const dim3 lgrid((unsigned)((2 * n + WPB * 32 - 1) / (WPB * 32)));
+        if (c->bk_ready) hipLaunchKernelGGL((refine_lane_kernel<32, true>), lgrid, block, 0, st, a);
+        else hipLaunchKernelGGL((refine_lane_kernel<32, false>), lgrid, block, 0, st, a);
         hipLaunchKernelGGL(refine_redo_kernel, dim3(8192), block, 0, st, a);   // ~1 left-over window per wave
     } else {
         hipLaunchKernelGGL(refine_span_kernel, grid, block, 0, st, a);
@@ -2327,6 +2446,7 @@ svt_status svt_open(const svt_params *params, int device, svt_ctx **out) {
     if (const char *x = getenv("SVTREK_IX")) c->ix_mode = strcmp(x, "lane") == 0 ? 1 : strcmp(x, "stream") == 0 ? 2 : 0;
     if (const char *x = getenv("SVTREK_IX_RANGES")) c->ix_ranges = std::max<uint64_t>(1, strtoull(x, nullptr, 10));
     if (const char *lw = getenv("SVTREK_LANE_W")) c->lane_w = atoi(lw) == 32 ? 32 : 0;
+    if (const char *x = getenv("SVTREK_INDEX")) c->bk_on = strcmp(x, "lists") != 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         delete c;
@@ -2411,7 +2531,7 @@ bool index_lane(const svt_ctx *c, uint64_t nops, uint64_t nreads) {
     return c->n_groups > 0 && (c->ix_mode == 1 || (c->ix_mode == 0 && nops <= 64ull * nreads));
 }
 
-svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
+IxArgs ix_args(const svt_ctx *c) {
     IxArgs a;
     a.stream = c->d_cigar;
     a.soff = c->d_off64;
@@ -2432,6 +2552,11 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     a.scrh = c->d_scrh;
     a.ovf = c->d_ovf;
     a.n_ranges = c->n_ranges;
+    return a;
+}
+
+svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
+    IxArgs a = ix_args(c);
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (ms)
         for (auto &e : ev) HIP_TRY(c, hipEventCreate(&e));
@@ -2500,6 +2625,115 @@ svt_status build_index(svt_ctx *c, hipStream_t st, bool first, double *ms) {
     return done(SVT_OK);
 }
 
+// ---- the value-bucketed event index (svt_bucket_build.inc): launch arguments, one pass, the
+// first build at load
+BkBuild bk_args(const svt_ctx *c, bool count, bool captured) {
+    BkBuild b{};
+    b.ev = c->d_bkev;
+    b.off = c->d_bkoff;
+    b.cur = count ? c->d_bkoff : captured ? c->d_bkcap : c->d_bkcur;
+    b.pmx = c->d_bkpm;
+    b.nbk = c->bk_n;
+    b.maxd = c->d_bkmaxd;
+    b.cbase = c->d_bkbase;
+    b.cnb = c->d_bknb;
+    b.k = count || captured ? 0u : c->bk_builds;
+    b.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
+    return b;
+}
+
+// One counting or filing pass on st: short reads walked from the CIGAR stream, long reads filed
+// from the span lists (which the caller rebuilt first).
+svt_status bk_pass(svt_ctx *c, hipStream_t st, bool count, bool captured) {
+    const IxArgs a = ix_args(c);
+    const BkBuild b = bk_args(c, count, captured);
+    const uint64_t nr = (uint64_t)c->n_reads;
+    if (index_lane(c, c->n_ops, nr)) {
+        const dim3 grid((unsigned)((c->n_groups + IXB_WPB - 1) / IXB_WPB)), block(64 * IXB_WPB);
+        if (count) hipLaunchKernelGGL(ixb_lane_kernel<true>, grid, block, 0, st, a, b, nr);
+        else hipLaunchKernelGGL(ixb_lane_kernel<false>, grid, block, 0, st, a, b, nr);
+    } else {
+        const dim3 grid((unsigned)((nr + IXB_T - 1) / IXB_T)), block(IXB_T);
+        if (count) hipLaunchKernelGGL(ixb_lists_kernel<true>, grid, block, 0, st, a, b, nr);
+        else hipLaunchKernelGGL(ixb_lists_kernel<false>, grid, block, 0, st, a, b, nr);
+    }
+    HIP_TRY(c, hipGetLastError());
+    return SVT_OK;
+}
+
+svt_status bk_check_err(svt_ctx *c) {
+    uint32_t e = 0;
+    HIP_TRY(c, hipDeviceSynchronize());
+    HIP_TRY(c, hipMemcpy(&e, c->d_ctl + 12, 4, hipMemcpyDeviceToHost));
+    if (e) {
+        HIP_TRY(c, hipMemset(c->d_ctl + 12, 0, 4));
+        return fail(c, SVT_EDEVICE, "%s", "device index build: the value buckets disagree with their count");
+    }
+    return SVT_OK;
+}
+
+// The first build (svt_load_pileup, after the span lists): buckets per contig from the largest
+// pos / endpos (values past them -- walks lengthened by H / P / N ops -- share the contig's last
+// bucket), the counting pass, the extents and prefix maxima on the host, the filing pass.  A pileup
+// whose events or buckets pass 2^32 keeps the span lists alone (bk_ready stays false).
+svt_status bk_load(svt_ctx *c, const std::vector<int64_t> &vtop) {
+    const int32_t nt = c->n_targets;
+    std::vector<uint64_t> cbase((size_t)nt);
+    std::vector<uint32_t> cnb((size_t)nt);
+    uint64_t NB = 0;
+    for (int32_t t = 0; t < nt; t++) {
+        const uint64_t nb = (((uint64_t)std::max<int64_t>(vtop[(size_t)t], 0) + 65536u) >> BKS) + 2u;
+        cbase[(size_t)t] = NB;
+        cnb[(size_t)t] = (uint32_t)nb;
+        NB += nb;
+    }
+    if (nt == 0 || NB >= 0xffffffffull) return SVT_OK;
+    svt_status s;
+    if ((s = upload(c, c->d_bkbase, cbase.data(), cbase.size()))) return s;
+    if ((s = upload(c, c->d_bknb, cnb.data(), cnb.size()))) return s;
+    if ((s = upload<uint32_t>(c, c->d_bkmaxd, nullptr, 0, (size_t)nt))) return s;
+    const uint64_t S1 = NB + 1;   // the tables' stride per array
+    if ((s = upload<uint32_t>(c, c->d_bkoff, nullptr, 0, BA_N * S1))) return s;   // (zeroed: the counts)
+    if ((s = upload<uint32_t>(c, c->d_bkcur, nullptr, 0, BA_N * S1))) return s;
+    if ((s = upload<uint32_t>(c, c->d_bkcap, nullptr, 0, (BA_N * S1 + 3) / 4 * 4))) return s;   // (whole uint4s: bk_zero_kernel)
+    if ((s = upload<int32_t>(c, c->d_bkpm, nullptr, 0, 3 * S1))) return s;
+    HIP_TRY(c, hipMemset(c->d_bkpm, 0xff, 3 * S1 * sizeof(int32_t)));   // -1: no key
+    c->bk_n = NB;
+    if ((s = bk_pass(c, nullptr, true, false)) || (s = bk_check_err(c))) return s;
+    // the extents: every array's buckets in order, the arrays one after the other in d_bkev
+    std::vector<uint32_t> cnt((size_t)(BA_N * S1));
+    std::vector<int32_t> pm((size_t)(3 * S1));
+    HIP_TRY(c, hipMemcpy(cnt.data(), c->d_bkoff, cnt.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(pm.data(), c->d_bkpm, pm.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t acc = 0;
+    for (int A = 0; A < BA_N; A++) {
+        const uint64_t a0 = acc;
+        uint32_t *o = cnt.data() + (size_t)A * S1;
+        for (uint64_t g = 0; g < NB; g++) {
+            const uint32_t x = o[(size_t)g];
+            o[(size_t)g] = (uint32_t)acc;
+            acc += x;
+            if (acc >= 0xffffffffull) return SVT_OK;   // (bk_ready stays false: the span lists alone)
+        }
+        o[(size_t)NB] = (uint32_t)acc;
+        c->bk_events[A] = acc - a0;
+        if (A < 3)   // the BELOW keys' prefix maxima, within each contig
+            for (int32_t t = 0; t < nt; t++) {
+                int32_t m = -1;
+                int32_t *q = pm.data() + (size_t)A * S1;
+                for (uint64_t g = cbase[(size_t)t], g1 = g + cnb[(size_t)t]; g < g1; g++) m = q[(size_t)g] = std::max(m, q[(size_t)g]);
+            }
+    }
+    HIP_TRY(c, hipMemcpy(c->d_bkoff, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_bkpm, pm.data(), pm.size() * 4, hipMemcpyHostToDevice));
+    if ((s = upload<uint4>(c, c->d_bkev, nullptr, 0, std::max<uint64_t>(acc, 1)))) return s;
+    c->bk_builds = 0;   // the cursors are zero: the first filing pass is epoch 0
+    if ((s = bk_pass(c, nullptr, false, false)) || (s = bk_check_err(c))) return s;
+    c->bk_builds = 1;
+    c->bk_ready = true;
+    return SVT_OK;
+}
+
 }  // namespace
 }  // extern "C++"
 
@@ -2522,6 +2756,7 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
     std::vector<uint4> rec((size_t)nr);
     std::vector<std::vector<uint2>> bk((size_t)nt);
     std::vector<const char *> bad((size_t)nt, nullptr);
+    std::vector<int64_t> vtop((size_t)nt, 0);   // per contig its largest pos / endpos (the value buckets)
     parallel_for((size_t)nt, 16, [&](size_t t) {
         const int64_t r0 = tid_off[t], r1 = tid_off[t + 1];
         if (r1 - r0 > 0xffffffffll) { bad[t] = "> 2^32 reads on one contig"; return; }
@@ -2537,11 +2772,12 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
             if (endpos[r] > m) m = endpos[r];
             maxpos = std::max(maxpos, pos[r]);
             emax[(size_t)r] = m;
-            rec[(size_t)r] = make_uint4((uint32_t)pos[r], (uint32_t)endpos[r], nc[r], 0u);
+            rec[(size_t)r] = make_uint4((uint32_t)pos[r], (uint32_t)endpos[r], nc[r], (uint32_t)t);   // .w: the contig
         }
         // bucket b = 0..nb-1: {first contig-relative read with pos >= b << BKT_SHIFT, first with
         // emax >= b << BKT_SHIFT}; the last bucket lies past every pos and endpos: {nr, nr}
         const int64_t top = r1 > r0 ? std::max<int64_t>(maxpos, m) : 0;
+        vtop[t] = top;
         const int64_t nb = (top >> BKT_SHIFT) + 2;
         std::vector<uint2> &B = bk[t];
         B.reserve((size_t)nb);
@@ -2646,6 +2882,19 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
             c->load_stats.index_bytes = 8ull * nstream + 65ull * R + 16ull * (c->n_evD + c->n_evI);
         else
             c->load_stats.index_bytes = 4ull * nstream + 56ull * R + 48ull * (c->n_evD + c->n_evI);
+        if (c->bk_on) {   // the value buckets, filed from the stream (short reads) or the span lists
+            if ((s = bk_load(c, vtop))) return s;
+            if (c->bk_ready) {
+                uint64_t placed = 0;
+                for (int A = 0; A < BA_N; A++) placed += c->bk_events[A];
+                c->load_stats.bucket_index = 1;
+                c->load_stats.buckets = c->bk_n;
+                c->load_stats.bucket_events = placed;
+                c->load_stats.bucket_bytes = c->load_stats.index_kind == 1
+                    ? 4ull * nstream + 24ull * R + 28ull * placed
+                    : c->load_stats.index_bytes + 32ull * R + 16ull * (c->n_evD + c->n_evI) + 28ull * placed;
+            }
+        }
     } else {
         for (auto *pp : {&c->d_spD, &c->d_spI})
             if ((s = upload<uint4>(c, *pp, nullptr, 0, 1))) return s;
@@ -2768,7 +3017,24 @@ svt_status svt_reindex(svt_ctx *c, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     svt_status s = order_on(c, st);   // after every launch already issued (they read the index)
     if (s) return s;
-    return build_index(c, st, false, nullptr);
+    if (!c->bk_ready) return build_index(c, st, false, nullptr);
+    // the value buckets: short reads filed straight from the CIGAR stream; long reads from the
+    // span lists, rebuilt first.  A captured build files through its own cursors (zeroed by the
+    // graph), a direct one through the epoch cursors (svt_bucket_build.inc).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (st) HIP_TRY(c, hipStreamIsCapturing(st, &cap));
+    const bool captured = cap == hipStreamCaptureStatusActive;
+    if (!index_lane(c, c->n_ops, (uint64_t)c->n_reads) && (s = build_index(c, st, false, nullptr))) return s;
+    if (captured)
+    {   // (the buffer is allocated in whole uint4s: upload's size below rounds it up)
+        const uint64_t n4 = (BA_N * (c->bk_n + 1) + 3) / 4;
+        hipLaunchKernelGGL(bk_zero_kernel, dim3((unsigned)std::min<uint64_t>((n4 + 255) / 256, 4096)), dim3(256), 0, st,
+                           reinterpret_cast<uint4 *>(c->d_bkcap), n4);
+        HIP_TRY(c, hipGetLastError());
+    }
+    if ((s = bk_pass(c, st, false, captured))) return s;
+    if (!captured) c->bk_builds++;
+    return SVT_OK;
 }
 
 svt_status svt_last_load_stats(const svt_ctx *c, svt_load_stats *out) {
@@ -2807,8 +3073,9 @@ svt_status svt_sync(svt_ctx *c, void *stream) {
     if (st2[1]) {   // the index build's guard fired: census and emit disagreed (an engine bug)
         HIP_TRY(c, hipMemset(c->d_ctl + 12, 0, 4));
         return fail(c, SVT_EDEVICE, "%s",
-                    st2[1] == 2 ? "device index build: a look-back never ended (results invalid)"
-                                : "device index build: emit overran the census's sizes (results invalid)");
+                    st2[1] == 2   ? "device index build: a look-back never ended (results invalid)"
+                    : st2[1] == 3 ? "device index build: an event outside its value bucket's extent (results invalid)"
+                                  : "device index build: emit overran the census's sizes (results invalid)");
     }
 #if SVT_DIAG == 9
     fprintf(stderr, "[diag] wave-wide (phase 3) windows: %d\n", status >> 8);
@@ -2852,8 +3119,14 @@ static svt_status run_batch_1(svt_ctx *c, const svt_locus *loci, size_t n, svt_r
         // bucket words per search pair, the search entries, the two span bounds of a query and
         // its 16-B events, per stop search the chunk words scanned, the word before the break
         // chunk and its 8 CIGAR words
+        w->bucket_queries = k[W_BQ];
+        w->bucket_events = k[W_BEV];
         w->event_bytes = 24ull * n + 32ull * w->queries + 4ull * w->probe_entries + 36ull * w->stop_searches +
                          4ull * w->stop_chunk_words + 16ull * w->span_bounds + 16ull * w->span_events;
+        // the value buckets (svt_bucket.inc): locus in + result out, per window two bucket offsets
+        // and one prefix-max key, the 16-B events of its band's buckets and of the walks for ABOVE
+        // (windows the buckets do not take -- none at the default parameters -- are not priced)
+        if (c->bk_ready) w->event_bytes = 24ull * n + 12ull * w->bucket_queries + 16ull * w->bucket_events;
     }
     return SVT_OK;
 }

@@ -112,10 +112,30 @@ def test_span_walk_counters(engine_factory):
     assert 0 < w["span_bounds"] <= w["queries"] <= w["windows"]
     assert w["span_events"] >= w["candidates"] * 0.5
     assert w["range_reads"] == 0 and w["list_entries"] == 0
+    assert eng.load_stats()["bucket_index"] == 1
+    # the value buckets (the default): every window of the default parameters is answered from them,
+    # reading its band's buckets (and, when the vote needs ABOVE, the bounded walks) -- a fraction of
+    # the span walk's events
+    assert 0.99 * w["queries"] <= w["bucket_queries"] <= w["queries"]
+    assert 0 < w["bucket_events"] < w["span_events"]
+    assert w["event_bytes"] == 24 * n + 12 * w["bucket_queries"] + 16 * w["bucket_events"]
+    assert w["event_bytes"] < 24 * n + 12 * w["reads"] + 4 * w["ops_walked"]
+    _same(eng.refine(r.loci), O.refine_batch(r.pileup, r.loci, threads=8))
+
+
+def test_span_list_counters(engine_factory):
+    """SVTREK_INDEX=lists (the span lists alone, rounds 1-5): no bucket counters, event_bytes the
+    span walk's own bytes, same results."""
+    r = _workload(n_loci=4000, seed=65)
+    eng = engine_factory(env={"SVTREK_INDEX": "lists"})
+    eng.load_pileup(r.pileup)
+    assert eng.load_stats()["bucket_index"] == 0
+    w = eng.count_work(r.loci)
+    n = len(r.loci)
+    assert w["bucket_queries"] == 0 and w["bucket_events"] == 0
     exp = (24 * n + 32 * w["queries"] + 4 * w["probe_entries"] + 36 * w["stop_searches"]
            + 4 * w["stop_chunk_words"] + 16 * w["span_bounds"] + 16 * w["span_events"])
     assert w["event_bytes"] == exp
-    assert w["event_bytes"] < 24 * n + 12 * w["reads"] + 4 * w["ops_walked"]
     _same(eng.refine(r.loci), O.refine_batch(r.pileup, r.loci, threads=8))
 
 
