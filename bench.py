@@ -186,7 +186,7 @@ def parity_sample(parts, res, first_rows, n_random: int = 10000, seed: int = 0, 
 STEP_KERNELS = ("ix2_census_kernel", "ix2_emit_kernel", "refine_lane_kernel", "refine_redo_kernel")
 STREAM_INDEX_KERNELS = ("index_kernel", "ix_copy_kernel")   # the long-read index build (svt_index.inc)
 BUCKET_INDEX_KERNELS = ("ixb_lane_kernel",)                  # the value buckets filed from the stream (short reads)
-BUCKET_STREAM_KERNELS = ("index_kernel", "ix_copy_kernel", "ixb_lists_kernel")   # ... from the span lists (long reads)
+BUCKET_STREAM_KERNELS = ("index_kernel", "ixb_copy_kernel")   # ... from the stream walk's stage (long reads)
 
 
 def index_kernels(load_stats: dict) -> tuple:
@@ -625,8 +625,9 @@ def main() -> int:
                              "index_bytes_def": ("value buckets (svt_load_stats.bucket_bytes): short reads, the CIGAR "
                                                  "stream once (4 B/op) + 24 B/read (offsets, record) + 28 B/filed event "
                                                  "(16-B event written, its bucket's two 4-B offsets read, 4-B cursor "
-                                                 "incremented; a D > 50 op is filed twice); long reads, the span lists' "
-                                                 "build + 32 B/read + 16 B/list event read + 28 B/filed event"
+                                                 "incremented; a D > 50 op is filed twice); long reads, the stream "
+                                                 "walk's stage: the stream once + 32 B/read + 32 B/staged event + 28 B/filed "
+                                                 "event"
                                                  if load_stats.get("bucket_index") else
                                                  "lane per read: CIGAR stream twice (4 B/op; census + emit), 65 B/read "
                                                  "(census soff, clip byte, counts; emit counts, soff, rec, offsets), 16 B/span "

@@ -303,8 +303,9 @@ typedef struct svt_load_stats {
     uint64_t bucket_bytes;  /* algorithmic bytes of one rebuild: lane per read, the CIGAR stream
                                once (4 B/op) + 24 B per read (offsets, record) + 28 B per filed
                                event (16-B event written, its bucket's two 4-B offsets read and
-                               4-B cursor incremented); long reads: the span-list build's bytes +
-                               16 B per list event read + 28 B per filed event                    */
+                               4-B cursor incremented); long reads (filed from the stream walk's
+                               stage): the stream once + 32 B per read + 32 B per staged event
+                               (written, read back) + 28 B per filed event                        */
 } svt_load_stats;
 svt_status svt_last_load_stats(const svt_ctx *ctx, svt_load_stats *out);
 

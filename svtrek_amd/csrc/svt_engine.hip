@@ -2652,10 +2652,12 @@ svt_status bk_pass(svt_ctx *c, hipStream_t st, bool count, bool captured) {
         const dim3 grid((unsigned)((c->n_groups + IXB_WPB - 1) / IXB_WPB)), block(64 * IXB_WPB);
         if (count) hipLaunchKernelGGL(ixb_lane_kernel<true>, grid, block, 0, st, a, b, nr);
         else hipLaunchKernelGGL(ixb_lane_kernel<false>, grid, block, 0, st, a, b, nr);
-    } else {
+    } else if (count) {   // (at load: the span lists the first build made)
         const dim3 grid((unsigned)((nr + IXB_T - 1) / IXB_T)), block(IXB_T);
-        if (count) hipLaunchKernelGGL(ixb_lists_kernel<true>, grid, block, 0, st, a, b, nr);
-        else hipLaunchKernelGGL(ixb_lists_kernel<false>, grid, block, 0, st, a, b, nr);
+        hipLaunchKernelGGL(ixb_lists_kernel<true>, grid, block, 0, st, a, b, nr);
+    } else {              // from the stream walk's stage (index_kernel ran just before on st)
+        const dim3 grid((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), block(64 * IX_WPB);
+        hipLaunchKernelGGL(ixb_copy_kernel, grid, block, 0, st, a, b);
     }
     HIP_TRY(c, hipGetLastError());
     return SVT_OK;
@@ -2892,7 +2894,7 @@ static svt_status load_core(svt_ctx *c, int32_t nt, const int64_t *tid_off, cons
                 c->load_stats.bucket_events = placed;
                 c->load_stats.bucket_bytes = c->load_stats.index_kind == 1
                     ? 4ull * nstream + 24ull * R + 28ull * placed
-                    : c->load_stats.index_bytes + 32ull * R + 16ull * (c->n_evD + c->n_evI) + 28ull * placed;
+                    : 4ull * nstream + 32ull * R + 32ull * (c->n_evD + c->n_evI) + 28ull * placed;
             }
         }
     } else {
@@ -3024,7 +3026,12 @@ svt_status svt_reindex(svt_ctx *c, void *stream) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (st) HIP_TRY(c, hipStreamIsCapturing(st, &cap));
     const bool captured = cap == hipStreamCaptureStatusActive;
-    if (!index_lane(c, c->n_ops, (uint64_t)c->n_reads) && (s = build_index(c, st, false, nullptr))) return s;
+    if (!index_lane(c, c->n_ops, (uint64_t)c->n_reads)) {   // long reads: the stream walk stages the events
+        const IxArgs a = ix_args(c);
+        hipLaunchKernelGGL(index_kernel, dim3((unsigned)((c->n_ranges + IX_WPB - 1) / IX_WPB)), dim3(64 * IX_WPB), 0, st, a);
+        HIP_TRY(c, hipGetLastError());
+        c->bsum_dirty = true;   // (its block sums are not scanned: the next span-list build clears them)
+    }
     if (captured)
     {   // (the buffer is allocated in whole uint4s: upload's size below rounds it up)
         const uint64_t n4 = (BA_N * (c->bk_n + 1) + 3) / 4;
