@@ -1399,16 +1399,28 @@ __device__ __forceinline__ void lane_walk2(const LwOne &A, const LwOne &B, uint1
 // s / e / band (the tests of span_cand_mask, per lane); members go to the window's row at
 // their rank among its members, and each window's first lane writes its meta row (band size,
 // candidates, below / above) -- everything lane_walk gives a window, for 1-64 events at once.
+// The event lane ln tests in the packed slot of windows win[c0..] with marks M (value buckets: one
+// event array) -- loaded ahead of the slot's tests so that a run of packed slots keeps the next
+// slot's loads in flight while the current one is tested.
+__device__ __forceinline__ uint4 lane_packed_load(const BkIndex &B, const LvWin *win, uint32_t c0, uint64_t M) {
+    const int ln = lane_id();
+    const uint64_t upto = M & ((2ull << ln) - 1ull);
+    const uint32_t r = (uint32_t)__popcll(upto) - 1u, f = 63u - (uint32_t)__clzll(upto);
+    const LvWin &w = win[c0 + r];
+    return B.ev[w.e0 + min((uint32_t)ln - f, w.len - 1u)];
+}
+
 template <bool BK>
 __device__ __forceinline__ void lane_packed(const DevPileup &P, const BkIndex &B, const LvWin *win, LvMeta *meta,
-                                            uint16_t *stage, uint32_t c0, uint64_t M, uint32_t tot, int32_t bw2) {
+                                            uint16_t *stage, uint32_t c0, uint64_t M, uint32_t tot, int32_t bw2,
+                                            const uint4 *vpre = nullptr) {
     const int ln = lane_id();
     const uint64_t upto = M & ((2ull << ln) - 1ull);   // marks at or below this lane (ln 63: all)
     const uint32_t r = (uint32_t)__popcll(upto) - 1u, f = 63u - (uint32_t)__clzll(upto);
     const LvWin w = win[c0 + r];
     const uint32_t kind = w.kl & 0xffu, k = w.kl >> 8;
     const uint4 *evb = (BK ? B.ev : kind == (uint32_t)K_INS ? P.spI : P.spD) + w.e0;
-    const uint4 v = evb[min((uint32_t)ln - f, w.len - 1u)];   // lanes past tot: their window's last event
+    const uint4 v = vpre ? *vpre : evb[min((uint32_t)ln - f, w.len - 1u)];   // lanes past tot: their window's last event
     const uint32_t s = w.s, e = w.e, x = v.x, op = v.y & 0xfu;
     const int32_t lo = w.lo;
     const uint64_t isI = ballot(kind == (uint32_t)K_INS), isE = ballot(kind == (uint32_t)K_END);
@@ -1815,8 +1827,38 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                 M |= 1ull << tot;
                 tot += l;
             }
-            lane_packed<BK>(a.pile, a.bk, L.win, L.meta, L.stage, c, M, tot, bw2);
-            c = c1;
+            if (!BK) {
+                lane_packed<BK>(a.pile, a.bk, L.win, L.meta, L.stage, c, M, tot, bw2);
+                c = c1;
+                continue;
+            }
+            // value buckets: most windows hold < 64 events, so a wave's phase 1 is a run of packed
+            // slots -- each slot's events are loaded while the previous slot is tested (the loads,
+            // not the tests, were the run's length: one round trip per slot, ~9 slots a wave on cfg4)
+            uint4 v = lane_packed_load(a.bk, L.win, c, M);
+            for (;;) {
+                uint64_t Mn = 1ull;
+                uint32_t totn = 0, cn1 = c1;
+                const bool more = c1 < nwin && rdlane(lenv, (int)c1) <= (uint32_t)WAVE;
+                if (more) {
+                    totn = rdlane(lenv, (int)c1);
+                    for (cn1 = c1 + 1u; cn1 < nwin; cn1++) {
+                        const uint32_t l = rdlane(lenv, (int)cn1);
+                        if (totn + l > (uint32_t)WAVE) break;
+                        Mn |= 1ull << totn;
+                        totn += l;
+                    }
+                }
+                // (unconditional: a load under a branch would be waited for at the join)
+                const uint4 vn = lane_packed_load(a.bk, L.win, more ? c1 : c, more ? Mn : M);
+                lane_packed<BK>(a.pile, a.bk, L.win, L.meta, L.stage, c, M, tot, bw2, &v);
+                c = c1;
+                if (!more) break;
+                v = vn;
+                M = Mn;
+                tot = totn;
+                c1 = cn1;
+            }
         }
         wave_sync();
     }
@@ -1867,20 +1909,38 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             else if (nmax <= 16) lv_oe_sort<0, 16>(x);
             else lv_oe_sort<0, 32>(x);
             uint32_t *wrow = reinterpret_cast<uint32_t *>(row);
-            // value buckets: ABOVE was only seen as far as the band's buckets; the vote reads it
-            // only when no candidate lies below pos - 25 (lane_vote's q) -- then the wave-wide path
-            // walks for it (bk_above, refine_redo_kernel)
-            const bool needA = BK && pend && !(mt.flags & (LV_BELOW | LV_ABOVE)) &&
-                               (int32_t)x[0] >= bw - SV_MIN_LENGTH / 2;
-            redo |= ballot(needA);
-            if (pend && !needA) {
+            int32_t l0 = 0;
+            if (pend) {
 #pragma unroll
                 for (int j = 0; j < LV_CAP; j += 2) wrow[j >> 1] = x[j] | x[j + 1] << 16;
                 // the band elements <= pos + 25, counted on the sorted registers (no search)
-                int32_t l0 = 0;
 #pragma unroll
                 for (int j = 0; j < LV_CAP; j++) l0 += (int32_t)(x[j] <= (uint32_t)(bw + SV_MIN_LENGTH / 2));
                 l0 = min(l0, nb);
+            }
+            // value buckets: ABOVE was only seen as far as the band's buckets; the vote reads it
+            // only when no candidate lies below pos - 25 (lane_vote's q) -- then the wave walks for
+            // it, window by window (bk_above: the bounded walks of svt_bucket.inc)
+            const bool needA = BK && pend && !(mt.flags & (LV_BELOW | LV_ABOVE)) &&
+                               (int32_t)x[0] >= bw - SV_MIN_LENGTH / 2;
+            if (BK) {
+                for (uint64_t na = ballot(needA); na; na &= na - 1ull) {
+                    const int l = __builtin_ctzll(na);
+                    uint32_t li, wi, ws = 0, we = 0, wimp = 0;
+                    int32_t chrom;
+                    const int kind = window_of(a, g0 + (uint32_t)l, li, wi, chrom, ws, we, wimp);
+                    BkWin W;
+                    bool ab = false;
+                    if (bk_eligible(a, kind, chrom, ws, we, wimp, W) == 1) {
+                        unsigned long long wk_ = 0;
+                        if (kind == K_INS) ab = bk_above<K_INS>(a.bk, chrom - 1, W, wk_);
+                        else if (kind == K_START) ab = bk_above<K_START>(a.bk, chrom - 1, W, wk_);
+                        else ab = bk_above<K_END>(a.bk, chrom - 1, W, wk_);
+                    }
+                    if (ln == l && ab) mt.flags |= LV_ABOVE;
+                }
+            }
+            if (pend) {
                 const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k, l0);
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
             }
