@@ -2106,6 +2106,7 @@ struct svt_ctx {
     uint32_t *d_bknb = nullptr;       // [n_targets] its buckets
     uint32_t *d_bkmaxd = nullptr;     // [n_targets] its longest D > 50 op
     uint32_t bk_builds = 0;           // filing passes so far (the cursors' epoch)
+    uint32_t bk_nev = 0;              // d_bkev's events (every array's)
     uint64_t dev_bytes = 0;
     bool loaded = false;
     svt_load_stats load_stats{};      // timings of the last svt_load_pileup
@@ -2212,7 +2213,7 @@ void free_pileup(svt_ctx *c) {
     hfree(c->d_bkoff); hfree(c->d_bkcur); hfree(c->d_bkcap); hfree(c->d_bkev); hfree(c->d_bkpm);
     for (int A = 0; A < BA_N; A++) c->bk_events[A] = 0;
     hfree(c->d_bkbase); hfree(c->d_bknb); hfree(c->d_bkmaxd);
-    c->bk_ready = false; c->bk_n = 0; c->bk_builds = 0;
+    c->bk_ready = false; c->bk_n = 0; c->bk_builds = 0; c->bk_nev = 0;
     c->insseq_loaded = false; c->n_ins = 0; c->n_ranges = 0;
     c->n_evD = c->n_evI = 0;
     c->loaded = false; c->dev_bytes = 0; c->n_reads = 0; c->n_ops = 0; c->n_targets = 0;
@@ -2698,6 +2699,7 @@ BkBuild bk_args(const svt_ctx *c, bool count, bool captured) {
     b.cbase = c->d_bkbase;
     b.cnb = c->d_bknb;
     b.k = count || captured ? 0u : c->bk_builds;
+    b.n_ev = c->bk_nev;
     b.err = (uint32_t *)(c->d_ctl + 12);   // sticky status word 2 (svt_sync reports it)
     return b;
 }
@@ -2789,6 +2791,7 @@ svt_status bk_load(svt_ctx *c, const std::vector<int64_t> &vtop) {
     HIP_TRY(c, hipMemcpy(c->d_bkoff, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_bkpm, pm.data(), pm.size() * 4, hipMemcpyHostToDevice));
     if ((s = upload<uint4>(c, c->d_bkev, nullptr, 0, std::max<uint64_t>(acc, 1)))) return s;
+    c->bk_nev = (uint32_t)acc;
     c->bk_builds = 0;   // the cursors are zero: the first filing pass is epoch 0
     if ((s = bk_pass(c, nullptr, false, false)) || (s = bk_check_err(c))) return s;
     c->bk_builds = 1;

@@ -516,3 +516,40 @@ def test_index_kinds_agree_with_saturating_walks(engine_factory, seed):
             eng.reindex()
             _assert_same(eng.refine(loci), want, loci)
     assert all(x == stats[0] for x in stats)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_lane_filing_stage_overflow(engine_factory, seed):
+    """The short-read filing pass stages a group's events in LDS (256 of them, svt_bucket_build.inc
+    IXB_EVCAP); a group with more -- here reads with ~8 D > 50 / I >= 50 ops each, ~500 events a
+    group -- files the rest through a second walk of the group, and a group whose reads lie in two
+    contigs files all of its events that way.  Lane index forced (SVTREK_IX=lane); same results as
+    the oracle, also after rebuilds (the cursors' epochs)."""
+    from svtrek_amd.pileup import from_reads
+    rng = np.random.default_rng(90 + seed)
+    rows = []
+    for t in range(2):
+        pos = 3000
+        for i in range(1500):
+            pos += int(rng.integers(0, 12))
+            ops = []
+            for _ in range(int(rng.integers(4, 12))):
+                ops.append((0, int(rng.integers(20, 300))))
+                ops.append((int(rng.choice([1, 2])), int(rng.integers(45, 200))))
+            ops.append((0, int(rng.integers(10, 200))))
+            if rng.random() < 0.4:
+                ops = [(4, int(rng.integers(1, 40)))] + ops
+            if rng.random() < 0.4:
+                ops = ops + [(4, int(rng.integers(1, 40)))]
+            rows.append((t, pos, ops))
+    pl = from_reads(2, rows)
+    hot = [int(x) for x in rng.integers(4000, 12000, size=8)]
+    loci = random_loci(rng, 600, 2, 15000, hot)
+    want = O.refine_batch(pl, loci)
+    eng = engine_factory(env={"SVTREK_IX": "lane"})
+    eng.load_pileup(pl)
+    assert eng.load_stats()["index_kind"] == 1
+    _assert_same(eng.refine(loci), want, loci)
+    for _ in range(2):
+        eng.reindex()
+        _assert_same(eng.refine(loci), want, loci)
