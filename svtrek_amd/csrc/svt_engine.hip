@@ -1923,7 +1923,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             // it, window by window (bk_above: the bounded walks of svt_bucket.inc)
             const bool needA = BK && pend && !(mt.flags & (LV_BELOW | LV_ABOVE)) &&
                                (int32_t)x[0] >= bw - SV_MIN_LENGTH / 2;
-            if (BK) {
+            if (BK && SVT_DIAG != 41 && SVT_DIAG != 43) {   // (41, 43: diagnostic builds, no ABOVE walks)
                 for (uint64_t na = ballot(needA); na; na &= na - 1ull) {
                     const int l = __builtin_ctzll(na);
                     uint32_t li, wi, ws = 0, we = 0, wimp = 0;
@@ -1940,7 +1940,9 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
                     if (ln == l && ab) mt.flags |= LV_ABOVE;
                 }
             }
-            if (pend) {
+            if (SVT_DIAG == 42 || SVT_DIAG == 43) {   // diagnostic builds: no vote (42), no vote or ABOVE walks (43)
+                if (pend) write_result(a, mt.liw >> 1, mt.liw & 1u, x[0] + (uint32_t)l0 + (uint32_t)needA);
+            } else if (pend) {
                 const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k, l0);
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
             }
