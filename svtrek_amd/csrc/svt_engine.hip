@@ -41,7 +41,7 @@
 #include "../../include/svtrek_gpu.h"
 #include "svt_bamrec.h"
 
-#define SVT_VERSION "svtrek_amd 0.24.0 (gfx950, value-bucketed event index filed by a lane-per-read walk, band + prefix-max facts, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
+#define SVT_VERSION "svtrek_amd 0.25.0 (gfx950, value-bucketed event index filed by a lane-per-read walk with a 9-B LDS stage, band + prefix-max facts, packed span walk fed by readlane, lane vote, BGZF inflate + BAM decode)"
 
 namespace {
 
@@ -372,6 +372,9 @@ __device__ __forceinline__ uint32_t ref_adv(uint32_t w) {   // refinement.c:141:
     return (w >> 4) & (uint32_t)__builtin_amdgcn_sbfe((int)~0x12u, w & 0xfu, 1);
 }
 
+#ifndef SVT_VOTE2
+#define SVT_VOTE2 0              // 1: a window's two vote passes in two lanes (parity-green, no faster: profiles/r06_AA)
+#endif
 #ifndef SVT_DIAG
 #define SVT_DIAG 0               // diagnostic builds only (wrong results): 1 = region query only, 3 = no refine_end
                                  // stop search, 4 = no sort/vote, 5 = sort + prefix sums, no vote, ...,
@@ -1553,6 +1556,54 @@ __device__ __forceinline__ int32_t lane_vote(const uint16_t *B, int32_t nb, int3
     return distL < distR ? valL : valR;                                      // :100
 }
 
+// One of lane_vote's two passes (right: the pass above pos - 25, refinement.c:78-98; else the
+// pass below pos + 25, :56-76), written once for both directions so that the two passes of a
+// window run in two lanes of one wave at once: i walks from the pass's start in direction dir,
+// and the cluster's far end f moves the same way while its next element lies within ci of
+// B[i].  Returns whether the pass returned early (val = that value); otherwise val / dist are
+// the pass's best (-1 / INT_MAX: none).
+__device__ __forceinline__ bool lane_vote_half(const uint16_t *B, int32_t nb, int32_t w, int32_t lo, uint32_t fl,
+                                               const KParams &k, int32_t l0, bool right, int32_t &val, int32_t &dist) {
+    const int32_t ci = k.ci, range = k.range;
+    const bool below = fl & LV_BELOW, above = fl & LV_ABOVE;
+    int32_t start;
+    if (!right) {
+        const bool u0 = !below && l0 == 0;
+        start = nb == 0 ? -1 : u0 ? 0 : l0 == 0 ? -1 : l0 - 1;
+    } else {
+        const bool lt = below || (nb > 0 && (int32_t)B[0] < w - SV_MIN_LENGTH / 2);
+        start = lt ? (!below ? 0 : nb) : (!above ? nb - 1 : nb);
+    }
+    const int32_t dir = right ? 1 : -1;
+    int32_t mx = k.min_count - 1, f = start - dir, prev = 0;
+    uint32_t S = 0;
+    val = -1;
+    dist = 0x7fffffff;
+    for (int32_t i = start; i >= 0 && i < nb; i += dir) {
+        const int32_t a = B[i];
+        if (ref_abs(w - a) >= range) break;
+        if (i != start) S -= (uint32_t)prev;                     // the element behind i leaves
+        if ((f - i) * dir < 0) { f = i; S = (uint32_t)a; }
+        for (;;) {                                               // :61-64 / :83-86
+            const int32_t g = f + dir;
+            if (g < 0 || g >= nb) break;
+            const int32_t b = B[g];
+            if ((b - a) * dir > ci) break;
+            f = g;
+            S += (uint32_t)b;
+        }
+        prev = a;
+        const int32_t c = (f - i) * dir + 1;
+        if (c > mx) {                                            // :67-76 / :88-97
+            const int32_t co = (int32_t)div_small(S + (uint32_t)(c / 2), (uint32_t)c);
+            const int32_t d = ref_abs(w - co);
+            if (d < ci) { val = lo + co; return true; }
+            if (d < dist) { mx = c; val = lo + co; dist = d; }
+        }
+    }
+    return false;
+}
+
 // A2 (audit.c:176-225) for window g: kind (-1: none -> NA), s, e, pos of the vote.
 __device__ __forceinline__ int window_of(const KArgs &a, uint32_t g, uint32_t &li, uint32_t &w, int32_t &chrom,
                                          uint32_t &s, uint32_t &e, uint32_t &imp) {
@@ -1942,6 +1993,22 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             }
             if (SVT_DIAG == 42 || SVT_DIAG == 43) {   // diagnostic builds: no vote (42), no vote or ABOVE walks (43)
                 if (pend) write_result(a, mt.liw >> 1, mt.liw & 1u, x[0] + (uint32_t)l0 + (uint32_t)needA);
+            } else if (SVT_VOTE2 && LV_W <= 32) {
+                // the two passes of window j in lanes j (below pos + 25) and j + 32 (above pos - 25)
+                const int src = ln & 31;
+                const bool right = ln >= 32;
+                const bool pv = __shfl((int)pend, src, WAVE) != 0;
+                const int32_t nbv = __shfl(nb, src, WAVE), lov = __shfl(mt.lo, src, WAVE), l0v = __shfl(l0, src, WAVE);
+                const uint32_t flv = (uint32_t)__shfl((int)mt.flags, src, WAVE);
+                int32_t val = -1, dist = 0x7fffffff;
+                bool early = false;
+                if (pv) early = lane_vote_half(L.stage + (uint32_t)src * LV_S, nbv, bw, lov, flv, k, l0v, right, val, dist);
+                const int32_t valR = __shfl(val, src + 32, WAVE), distR = __shfl(dist, src + 32, WAVE);
+                const bool earlyR = __shfl((int)early, src + 32, WAVE) != 0;
+                if (pend) {   // :100 after an early return of neither pass
+                    const int32_t r = early ? val : earlyR ? valR : dist < distR ? val : valR;
+                    write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);
+                }
             } else if (pend) {
                 const int32_t r = lane_vote(row, nb, bw, mt.lo, mt.flags, k, l0);
                 write_result(a, mt.liw >> 1, mt.liw & 1u, (uint32_t)r);

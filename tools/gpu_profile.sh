@@ -21,6 +21,8 @@ step() {  # name, timeout, cmd...
 B=(python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-cold "${ARGS[@]}")
 step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-cold "${ARGS[@]}"
+step trace1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace1" -o run -- \
+  python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-cold --inflight 1 "${ARGS[@]}"
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- "${B[@]}"
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- "${B[@]}"
 step pmc_rdreq 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \

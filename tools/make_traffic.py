@@ -40,6 +40,8 @@ STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's
     "ix_scan_blocks_kernel": "ix_scan_blocks_kernel",
     "index_kernel": "(anonymous namespace)::index_kernel(",
     "ix_copy_kernel": "ix_copy_kernel",
+    "ixb_lane_kernel": "ixb_lane_kernel<false>",   # value buckets: the short-read filing pass
+    "ixb_copy_kernel": "ixb_copy_kernel",          # ... the long reads' stage filed
     "refine_lane_kernel": "refine_lane_kernel",
     "refine_span_kernel": "refine_span_kernel",   # (the engine's pick below 64K windows: cfg1, cfg2)
     "refine_redo_kernel": "refine_redo_kernel",
@@ -47,14 +49,29 @@ STEP = {   # the kernels of one bench.py step (label -> substring of rocprofv3's
 
 
 def kernel_avg_ns(src: str, kernel: str) -> float | None:
-    """Average duration of the kernel in the run's rocprofv3 --stats summary (trace/)."""
-    path = os.path.join(src, "trace", "run_kernel_stats.csv")
+    """Average duration of the kernel in the run's rocprofv3 --stats summary: the one-step-in-flight
+    trace (trace1/: no other step's kernels beside it) when the run has one, else trace/."""
+    path = os.path.join(src, "trace1", "run_kernel_stats.csv")
+    if not os.path.exists(path):
+        path = os.path.join(src, "trace", "run_kernel_stats.csv")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         for r in csv.DictReader(f):
             if kernel in r["Name"]:
                 return float(r["AverageNs"])
+    return None
+
+
+def kernel_calls(src: str, kernel: str) -> int | None:
+    """Launches of the kernel in the traced run (trace/run_kernel_stats.csv)."""
+    path = os.path.join(src, "trace", "run_kernel_stats.csv")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r["Name"]:
+                return int(r["Calls"])
     return None
 
 
@@ -95,14 +112,26 @@ def main() -> int:
     ap.add_argument("--workload", default="cfg4_1m_delins_30x_hifi")
     a = ap.parse_args()
     os.makedirs(a.dst, exist_ok=True)
-    copies = {"trace/run_kernel_stats.csv": "kernel_stats.csv", "pmc_fetch/run_counter_collection.csv":
+    copies = {"trace/run_kernel_stats.csv": "kernel_stats.csv", "trace1/run_kernel_stats.csv": "kernel_stats_inflight1.csv",
+              "trace1.log": "bench_under_rocprof_inflight1.log", "pmc_fetch/run_counter_collection.csv":
               "pmc_fetch_size.csv", "pmc_write/run_counter_collection.csv": "pmc_write_size.csv",
               "pmc_rdreq/run_counter_collection.csv": "pmc_rdreq.csv",
               "pmc_dram/run_counter_collection.csv": "pmc_dram.csv", "pmc_sq/run_counter_collection.csv": "pmc_sq.csv",
               "trace.log": "bench_under_rocprof.log"}
     for s_, d in copies.items():
-        if os.path.exists(os.path.join(a.src, s_)):
-            shutil.copy(os.path.join(a.src, s_), os.path.join(a.dst, d))
+        sp = os.path.join(a.src, s_)
+        if not os.path.exists(sp):
+            continue
+        if s_.startswith("pmc_"):   # the engine's kernels only (the run's torch / runtime copies dropped)
+            with open(sp) as f, open(os.path.join(a.dst, d), "w", newline="") as g:
+                rd = csv.reader(f)
+                wr = csv.writer(g)
+                hdr = next(rd)
+                wr.writerow(hdr)
+                kn = hdr.index("Kernel_Name")
+                wr.writerows(r for r in rd if "anonymous namespace" in r[kn])
+        else:
+            shutil.copy(sp, os.path.join(a.dst, d))
     ver = None
     with open(os.path.join(a.src, "trace.log")) as f:
         for line in f:
@@ -110,10 +139,14 @@ def main() -> int:
                 ver = json.loads(line).get("engine_version", ver)
     new = []
     step = {"read_bytes_per_launch": 0, "write_bytes_per_launch": 0, "hbm_bytes_per_launch": 0}
+    calls = {label: kernel_calls(a.src, sub) for label, sub in STEP.items()}
+    per_step = max([calls.get("refine_lane_kernel") or 0, calls.get("refine_span_kernel") or 0])
     for label, sub in STEP.items():
         kb = kernel_bytes(a.src, sub)
         if kb is None:
             continue
+        if per_step and (calls.get(label) or 0) * 2 < per_step:
+            continue   # a load-time kernel (e.g. the span lists built once beside the value buckets)
         ns = kernel_avg_ns(a.src, sub)
         e = {"kernel": label, "records": True, "workload": a.workload, "engine_version": ver, **kb,
              "avg_ns": ns, "source": f"{a.dst}/pmc_*.csv, {a.dst}/kernel_stats.csv"}
