@@ -1070,7 +1070,10 @@ constexpr int WPB = 4;
 
 // The refine kernels are held to 64 VGPRs = 8 waves per SIMD (the CU's maximum): their walks
 // are bound by dependent-load latency, so resident waves are what hide it.
-#define SVT_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
+#ifndef SVT_REFINE_WAVES
+#define SVT_REFINE_WAVES 8
+#endif
+#define SVT_OCC __attribute__((amdgpu_waves_per_eu(SVT_REFINE_WAVES, SVT_REFINE_WAVES)))
 template <bool COUNT, int G>
 __device__ __forceinline__ void refine_body(const KArgs &a);
 
