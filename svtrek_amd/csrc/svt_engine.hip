@@ -1730,9 +1730,15 @@ __device__ __forceinline__ void lane_query_bk(const KArgs &a, uint32_t g, LvQuer
 #ifndef SVT_PHASE_PROF
 #define SVT_PHASE_PROF 0
 #endif
+// PH(...) / PH_T(t): the instrumentation's statements, compiled out of the product.
 #if SVT_PHASE_PROF
 __device__ unsigned long long ph_prof[16];
 #define PH_ADD(i, v) atomicAdd(&ph_prof[i], (unsigned long long)(v))
+#define PH(...) __VA_ARGS__
+#define PH_T(t) const long long t = wall_clock64()
+#else
+#define PH(...)
+#define PH_T(t)
 #endif
 template <int LV_W, bool BK>
 __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) {
@@ -1745,9 +1751,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
     const KParams &k = a.prm;
     const uint32_t cnt = min((uint32_t)LV_W, nw - g0);
     const int32_t bw = k.range + max(k.ci, 0);   // the band's half-width
-#if SVT_PHASE_PROF
-    const long long pt0 = wall_clock64();
-#endif
+    PH_T(pt0);
     const bool band_ok = k.range > SV_MIN_LENGTH / 2 && bw <= LV_WMAX && k.ci >= -LV_WMAX &&
                          SVT_DIAG != 7;
     // ---- phase 0: every window's A2 + A3 at once, one lane each (the dependent loads of
@@ -1789,9 +1793,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         nwin = (uint32_t)__popcll(wm);
     }
     wave_sync();
-#if SVT_PHASE_PROF
-    const long long pt1 = wall_clock64();
-#endif
+    PH_T(pt1);
     if (SVT_DIAG == 6) {   // diagnostic build: phase 0 only (its answers written out, so it is not dead code)
         if ((uint32_t)ln < cnt) {
             const LvMeta mt = L.meta[ln];
@@ -1819,19 +1821,10 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             wv.e0);
         uint16_t *sink = reinterpret_cast<uint16_t *>(&L.sink[ln]);
         const int32_t bw2 = 2 * bw;
-#if SVT_PHASE_PROF
-        if (ln == 0) PH_ADD(8, nwin);
-        {
-            const uint32_t tl = rdlane(wave_scan_add(lenv), WAVE - 1);
-            if (ln == 0) PH_ADD(9, tl);
-        }
-#endif
+        PH({ const uint32_t tl = rdlane(wave_scan_add(lenv), WAVE - 1); if (ln == 0) { PH_ADD(8, nwin); PH_ADD(9, tl); } })
         for (uint32_t c = 0; c < nwin;) {
             const uint32_t l0 = rdlane(lenv, (int)c);
-#if SVT_PHASE_PROF
-            if (ln == 0 && l0 > (uint32_t)WAVE) { PH_ADD(10, 1); PH_ADD(11, (l0 + 255u) / 256u); }
-            if (ln == 0 && l0 <= (uint32_t)WAVE) PH_ADD(12, 1);
-#endif
+            PH(if (ln == 0) { if (l0 > (uint32_t)WAVE) { PH_ADD(10, 1); PH_ADD(11, (l0 + 255u) / 256u); } else PH_ADD(12, 1); })
             if (l0 > (uint32_t)WAVE && l0 <= 2u * WAVE && c + 1u < nwin) {   // a pair of 2-slot windows?
                 const uint32_t l1 = rdlane(lenv, (int)(c + 1u));
                 const uint32_t ka = rdlane(klv, (int)c), kb = rdlane(klv, (int)(c + 1u));
@@ -1916,9 +1909,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
-#if SVT_PHASE_PROF
-    const long long pt2 = wall_clock64();
-#endif
+    PH_T(pt2);
     const bool mine = (uint32_t)ln < cnt;
     LvMeta mt = mine ? L.meta[ln] : LvMeta{0, 0, 0, 0};
     if (aflags) mt.flags = aflags;   // the window was walked alone
@@ -1956,9 +1947,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
             int32_t nmax = nb;   // wave max of nb: the smallest network that sorts every lane
 #pragma unroll
             for (int d = 32; d > 0; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
-#if SVT_PHASE_PROF
-            if (ln == 0) PH_ADD(nmax <= 8 ? 13 : nmax <= 16 ? 14 : 15, 1);
-#endif
+            PH(if (ln == 0) PH_ADD(nmax <= 8 ? 13 : nmax <= 16 ? 14 : 15, 1));
             if (nmax <= 8) lv_oe_sort<0, 8>(x);
             else if (nmax <= 16) lv_oe_sort<0, 16>(x);
             else lv_oe_sort<0, 32>(x);
@@ -2019,9 +2008,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         }
         wave_sync();
     }
-#if SVT_PHASE_PROF
-    const long long pt3 = wall_clock64();
-#endif
+    PH_T(pt3);
     // ---- the windows voted wave-wide go to refine_redo_kernel (rare: 0.6 % of cfg4's)
     if (SVT_DIAG == 11) {   // diagnostic build: each left-over window's result = 0xF0000000 | its reason
         if ((redo >> ln) & 1ull) write_result(a, mt.liw >> 1, mt.liw & 1u, 0xF0000000u | (mt.flags >> 16));
@@ -2037,12 +2024,7 @@ __global__ __launch_bounds__(64 * WPB) SVT_OCC void refine_lane_kernel(KArgs a) 
         base = rdlane(base, 0);
         if ((redo >> ln) & 1ull) a.redo_list[base + mbcnt(redo)] = g0 + (uint32_t)ln;
     }
-#if SVT_PHASE_PROF
-    if (ln == 0) {
-        const long long pt4 = wall_clock64();
-        PH_ADD(0, pt1 - pt0); PH_ADD(1, pt2 - pt1); PH_ADD(2, pt3 - pt2); PH_ADD(3, pt4 - pt3); PH_ADD(4, 1);
-    }
-#endif
+    PH(if (ln == 0) { const long long pt4 = wall_clock64(); PH_ADD(0, pt1 - pt0); PH_ADD(1, pt2 - pt1); PH_ADD(2, pt3 - pt2); PH_ADD(3, pt4 - pt3); PH_ADD(4, 1); })
 }
 
 // The lane kernel's left-over windows (band off, > LV_CAP band elements, > CAP candidates,
