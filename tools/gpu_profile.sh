@@ -31,4 +31,5 @@ step pmc_dram 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_
   --output-format csv -d "$OUT/pmc_dram" -o run -- "${B[@]}"
 step pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
   SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc_sq" -o run -- "${B[@]}"
+python tools/trim_prof.py "$OUT"   # (under gpurun's 64 MiB copy-back cap: no per-dispatch traces, engine kernels only)
 echo "profile $TAG done"
